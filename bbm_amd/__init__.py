@@ -1,0 +1,24 @@
+"""bbm_amd -- an MI355X-native (gfx950) batched BSDF backbone for bsdfbenchmark/bbm.
+
+The hot path of BBM -- bsdfmodel<>::eval / pdf / sample over many (in, out) direction pairs --
+runs in libbbm_hip.so (hand-written HIP kernels, C-ABI in include/bbm_hip.h).  This package is
+the host-side mirror of the reference's model interface: one constructor per exported model
+name, `fromString` / `bsdf_import`, `bsdf_flag`, `unit_t`, `BsdfSample`, and batched
+`eval` / `pdf` / `eval_pdf` / `sample` on torch CUDA tensors.
+
+Importing the package loads the HIP library; if it is missing the import fails loudly.
+"""
+from . import _lib
+from .backbone import (BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString, model_names,
+                       unit_t, _make_ctor)
+from .models import ATTRIBUTES
+
+_lib.load()
+
+__all__ = ["BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
+           "fill_directions", "ATTRIBUTES"]
+
+for _name in model_names():
+    globals()[_name] = _make_ctor(_name)
+    __all__.append(_name)
+del _name

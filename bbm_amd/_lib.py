@@ -1,0 +1,78 @@
+"""ctypes binding of libbbm_hip.so (C-ABI: include/bbm_hip.h).
+
+The library is built in-tree by __graft_entry__.build() (hipcc --offload-arch=gfx950) into
+bbm_amd/lib/libbbm_hip.so.  There is no fallback: if the library is missing or fails to load,
+every entry point raises, so a GPU run can never silently take a CPU path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbbm_hip.so")
+
+# return codes (include/bbm_hip.h)
+OK = 0
+ERR_INVALID_MODEL = -1
+ERR_INVALID_ARG = -2
+ERR_UNSUPPORTED = -3
+ERR_HIP = -4
+
+# exported symbols and their signatures: (restype, argtypes)
+_P = ctypes.c_void_p
+_F = ctypes.c_float
+_I = ctypes.c_int
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_SZ = ctypes.c_size_t
+
+SIGNATURES = {
+    "bbm_hip_abi_version": (_I, []),
+    "bbm_hip_last_error": (ctypes.c_char_p, []),
+    "bbm_hip_num_models": (_I, []),
+    "bbm_hip_model_name": (ctypes.c_char_p, [_I]),
+    "bbm_hip_model_id": (_I, [ctypes.c_char_p]),
+    "bbm_hip_model_nparams": (_I, [_I]),
+    "bbm_hip_model_params": (_I, [_I, _I, _P, _I]),
+    "bbm_hip_model_components": (_I, [_I]),
+    "bbm_hip_eval": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
+    "bbm_hip_pdf": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P]),
+    "bbm_hip_eval_pdf": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
+    "bbm_hip_sample": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "bbm_hip_fill_directions": (_I, [_U64, _U32, _U64, _SZ, _I, _P, _P, _P, _P]),
+}
+
+
+class BackboneError(RuntimeError):
+    """Raised when a libbbm_hip call fails (the reference throws std::runtime_error /
+    std::invalid_argument, include/core/error.h:42-46)."""
+
+    def __init__(self, code, message):
+        super().__init__(f"libbbm_hip error {code}: {message}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises if the HIP library is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(code):
+    """Turn a negative return code into BackboneError with the library's message."""
+    if code < 0:
+        msg = load().bbm_hip_last_error()
+        raise BackboneError(code, msg.decode() if msg else "")
+    return code

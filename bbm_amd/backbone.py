@@ -1,0 +1,320 @@
+"""Batched BSDF models over device memory -- the Python face of the HIP backbone.
+
+Mirrors the reference's runtime model handle (bsdf_ptr, include/bbm/bsdf_ptr.h:21-165, exposed
+to Python as BsdfPtr with eval / sample / pdf / reflectance, include/python/py_core.h:106-112),
+but every call takes N direction pairs at once instead of one:
+
+  * directions: a float32 CUDA tensor of shape (3, N) (rows x, y, z -- SoA) or a 3-tuple of
+    1-D float32 CUDA tensors;
+  * component / unit: bsdf_flag / unit_t, uniform per call (include/bbm/bsdf_flag.h,
+    include/bbm/unit.h);
+  * mask: optional bool/uint8 tensor of N lanes (the reference's `Mask mask=true`).
+
+All work runs in libbbm_hip (hand-written gfx950 kernels) on the current torch stream; this
+module only allocates outputs and passes pointers.  There is no CPU fallback.
+"""
+import ctypes
+import enum
+import re
+
+import numpy as np
+
+from . import _lib
+from .models import ATTRIBUTES, attr_size, nparams, to_string
+
+
+class bsdf_flag(enum.IntFlag):
+    """include/bbm/bsdf_flag.h:21-27"""
+    None_ = 0
+    Diffuse = 1
+    Specular = 2
+    All = 3
+
+
+class unit_t(enum.IntEnum):
+    """include/bbm/unit.h:20-24"""
+    Radiance = 0
+    Importance = 1
+
+
+class BsdfSample:
+    """bsdfsample (include/bbm/bsdfsample.h:20-25), batched: direction (3, N), pdf (N,), flag (N,)."""
+
+    def __init__(self, direction, pdf, flag):
+        self.direction, self.pdf, self.flag = direction, pdf, flag
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _soa(t, n=None, what="direction"):
+    """Return (x_ptr, y_ptr, z_ptr, n) for a (3, N) tensor or a tuple of three 1-D tensors."""
+    torch = _torch()
+    if isinstance(t, (tuple, list)):
+        rows = list(t)
+    else:
+        if t.dim() != 2 or t.shape[0] != 3:
+            raise ValueError(f"{what}: expected a (3, N) tensor, got {tuple(t.shape)}")
+        rows = [t[0], t[1], t[2]]
+    for r in rows:
+        if not isinstance(r, torch.Tensor) or r.dtype != torch.float32 or not r.is_cuda:
+            raise TypeError(f"{what}: expected float32 CUDA tensors")
+        if r.dim() != 1 or r.stride(0) != 1:
+            raise ValueError(f"{what}: rows must be contiguous 1-D tensors")
+    m = rows[0].numel()
+    if any(r.numel() != m for r in rows):
+        raise ValueError(f"{what}: x/y/z lengths differ")
+    if n is not None and m != n:
+        raise ValueError(f"{what}: expected {n} elements, got {m}")
+    return rows[0].data_ptr(), rows[1].data_ptr(), rows[2].data_ptr(), m
+
+
+def _mask_ptr(mask, n):
+    if mask is None:
+        return None, None
+    torch = _torch()
+    if mask.dtype == torch.bool:
+        mask = mask.view(torch.uint8)
+    if mask.dtype != torch.uint8 or not mask.is_cuda or mask.numel() != n:
+        raise TypeError("mask: expected a bool/uint8 CUDA tensor with one entry per pair")
+    mask = mask.contiguous()
+    return mask.data_ptr(), mask
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def model_names():
+    """Models available in the loaded HIP library (BBM_EXPORT_BSDFMODEL registry equivalent)."""
+    lib = _lib.load()
+    return [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
+
+
+def _model_params(model_id, which):
+    lib = _lib.load()
+    k = _lib.check(lib.bbm_hip_model_nparams(model_id))
+    buf = (ctypes.c_float * max(k, 1))()
+    _lib.check(lib.bbm_hip_model_params(model_id, which, buf, k))
+    return np.array(buf[:k], dtype=np.float32)
+
+
+class BsdfModel:
+    """One parameterised BSDF model, evaluated in batches on the GPU."""
+
+    def __init__(self, name, *args, **kwargs):
+        lib = _lib.load()
+        if name not in ATTRIBUTES:
+            raise ValueError(f"unknown BSDF model: {name}")
+        mid = lib.bbm_hip_model_id(name.encode())
+        if mid < 0:
+            raise _lib.BackboneError(mid, f"model {name} is not available in libbbm_hip")
+        self.name = name
+        self.model_id = mid
+        self._params = _model_params(mid, 0)
+        layout = ATTRIBUTES[name]
+        if len(args) > len(layout):
+            raise TypeError(f"{name}: too many positional attributes")
+        values = dict(zip([a for a, _ in layout], args))
+        for k, v in kwargs.items():
+            if k not in dict(layout):
+                raise TypeError(f"{name}: unknown attribute '{k}'")
+            if k in values:
+                raise TypeError(f"{name}: attribute '{k}' given twice")
+            values[k] = v
+        for k, v in values.items():
+            self.set_attribute(k, v)
+
+    # ---------------------------------------------------------------- attributes
+    def _slot(self, attr):
+        k = 0
+        for a, shape in ATTRIBUTES[self.name]:
+            if a == attr:
+                return k, shape
+            k += attr_size(shape)
+        raise KeyError(attr)
+
+    def set_attribute(self, attr, value):
+        k, shape = self._slot(attr)
+        n = attr_size(shape)
+        v = np.asarray(value, dtype=np.float32).reshape(-1)
+        if v.size == 1 and n > 1:      # a scalar broadcasts over an RGB / Vec2d attribute
+            v = np.repeat(v, n)
+        if v.size != n:
+            raise ValueError(f"{self.name}.{attr}: expected {n} values, got {v.size}")
+        self._params[k:k + n] = v
+
+    def attribute(self, attr):
+        k, shape = self._slot(attr)
+        v = self._params[k:k + attr_size(shape)].copy()
+        return v[0] if shape == () else v.reshape(shape)
+
+    def parameter_values(self):
+        """Flat parameter vector (bbm::parameter_values, include/bbm/bsdf_enumerate.h)."""
+        return self._params.copy()
+
+    def set_parameter_values(self, values):
+        v = np.asarray(values, dtype=np.float32).reshape(-1)
+        if v.size != self._params.size:
+            raise ValueError(f"{self.name}: expected {self._params.size} parameters, got {v.size}")
+        self._params[:] = v
+
+    def parameter_default_values(self):
+        return _model_params(self.model_id, 0)
+
+    def parameter_lower_bound(self):
+        return _model_params(self.model_id, 1)
+
+    def parameter_upper_bound(self):
+        return _model_params(self.model_id, 2)
+
+    def __str__(self):
+        return to_string(self.name, self._params)
+
+    __repr__ = __str__
+
+    # ---------------------------------------------------------------- batched evaluation
+    def _pptr(self):
+        return self._params.ctypes.data_as(ctypes.c_void_p)
+
+    def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
+                 rgb=None, pdf=None, stream=None, mode=3):
+        torch = _torch()
+        ix, iy, iz, n = _soa(in_, what="in")
+        ox, oy, oz, _ = _soa(out, n, what="out")
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        if mode & 1 and rgb is None:
+            rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
+        if mode & 2 and pdf is None:
+            pdf = torch.empty((n,), dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        s = _stream_ptr(stream)
+        if mode == 3:
+            rc = lib.bbm_hip_eval_pdf(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+                                      int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),
+                                      rgb[2].data_ptr(), pdf.data_ptr(), s)
+        elif mode == 1:
+            rc = lib.bbm_hip_eval(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+                                  int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(), rgb[2].data_ptr(), s)
+        else:
+            rc = lib.bbm_hip_pdf(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+                                 int(component), int(unit), pdf.data_ptr(), s)
+        _lib.check(rc)
+        return rgb, pdf
+
+    def eval(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, **kw):
+        """Spectrum eval(in, out, component, unit, mask) for N pairs -> (3, N) RGB."""
+        return self.eval_pdf(in_, out, component, unit, mask, mode=1, **kw)[0]
+
+    def pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, **kw):
+        """Value pdf(in, out, component, unit, mask) for N pairs -> (N,)."""
+        return self.eval_pdf(in_, out, component, unit, mask, mode=2, **kw)[1]
+
+    def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
+        """BsdfSample sample(out, xi, component, unit, mask) for N (out, xi) -> BsdfSample."""
+        torch = _torch()
+        ox, oy, oz, n = _soa(out, what="out")
+        if isinstance(xi, (tuple, list)):
+            x0, x1 = xi
+        else:
+            if xi.dim() != 2 or xi.shape[0] != 2:
+                raise ValueError("xi: expected a (2, N) tensor")
+            x0, x1 = xi[0], xi[1]
+        for x in (x0, x1):
+            if x.dtype != torch.float32 or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
+                raise TypeError("xi: expected float32 CUDA rows with one entry per direction")
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = x0.device
+        d = torch.empty((3, n), dtype=torch.float32, device=dev)
+        p = torch.empty((n,), dtype=torch.float32, device=dev)
+        f = torch.empty((n,), dtype=torch.int32, device=dev)
+        lib = _lib.load()
+        _lib.check(lib.bbm_hip_sample(self.model_id, self._pptr(), self._params.size, ox, oy, oz,
+                                      x0.data_ptr(), x1.data_ptr(), mptr, n, int(component), int(unit),
+                                      d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
+                                      _stream_ptr(stream)))
+        return BsdfSample(d, p, f)
+
+
+# ------------------------------------------------------------------------- string import
+
+_TOKEN = re.compile(r"\s*([A-Za-z_][A-Za-z0-9_]*|[-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?|[()\[\],=])")
+
+
+def _tokenize(s):
+    pos, out = 0, []
+    s = s.strip()
+    while pos < len(s):
+        m = _TOKEN.match(s, pos)
+        if not m:
+            raise ValueError(f"cannot parse BSDF string at: {s[pos:]!r}")
+        out.append(m.group(1))
+        pos = m.end()
+    return out
+
+
+def _parse_value(tok, i):
+    if tok[i] == "[":
+        vals, i = [], i + 1
+        while tok[i] != "]":
+            v, i = _parse_value(tok, i)
+            vals.append(v)
+            if tok[i] == ",":
+                i += 1
+        return vals, i + 1
+    return float(tok[i]), i + 1
+
+
+def fromString(s):
+    """Construct a model from its bbm::toString form, e.g. 'CookTorrance(albedo = [0.5, 0.5, 0.5],
+    roughness = 0.1, eta = 1.3)' (bsdf_string_convert.h:52-82 / bsdf_import.h:22-26).  Attributes
+    may appear in any order; missing ones keep their defaults."""
+    tok = _tokenize(s)
+    name = tok[0]
+    if name not in ATTRIBUTES:
+        raise ValueError(f"unknown BSDF model: {name}")
+    m = BsdfModel(name)
+    if len(tok) == 1:
+        return m
+    if tok[1] != "(" or tok[-1] != ")":
+        raise ValueError(f"malformed BSDF string: {s!r}")
+    i, layout, pos_idx = 2, [a for a, _ in ATTRIBUTES[name]], 0
+    while tok[i] != ")":
+        if i + 1 < len(tok) and tok[i + 1] == "=":
+            attr = tok[i]
+            v, i = _parse_value(tok, i + 2)
+        else:
+            attr = layout[pos_idx]
+            v, i = _parse_value(tok, i)
+        pos_idx += 1
+        m.set_attribute(attr, np.asarray(v, dtype=np.float32))
+        if tok[i] == ",":
+            i += 1
+    return m
+
+
+bsdf_import = fromString
+
+
+def _make_ctor(name):
+    def ctor(*args, **kwargs):
+        return BsdfModel(name, *args, **kwargs)
+    ctor.__name__ = name
+    ctor.__doc__ = f"Constructs: {name}({', '.join(a for a, _ in ATTRIBUTES[name])}) -- {nparams(name)} parameters"
+    return ctor
+
+
+def fill_directions(seed, stream_id, offset, n, mode=0, out=None, stream=None):
+    """Counter-based synthetic directions (bbm_hip_fill_directions) -> (3, n) float32 CUDA tensor."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty((3, n), dtype=torch.float32, device=torch.device("cuda", torch.cuda.current_device()))
+    lib = _lib.load()
+    _lib.check(lib.bbm_hip_fill_directions(seed, stream_id, offset, n, mode, out[0].data_ptr(), out[1].data_ptr(),
+                                           out[2].data_ptr(), _stream_ptr(stream)))
+    return out

@@ -1,0 +1,368 @@
+// bbm_amd/csrc/bbm_hip.hip -- libbbm_hip.so: streaming kernels, model registry and the C-ABI
+// declared in include/bbm_hip.h.
+//
+// Layout and launch: directions are SoA float32 in HBM; one thread owns four
+// consecutive pairs, so each lane issues one 16-byte load per input array (6 x dwordx4) and one
+// 16-byte store per output array -- every wave instruction moves a full 1 KiB, coalesced.  The
+// grid is a grid-stride loop capped at 8 workgroups of 256 threads per CU (2048 workgroups on
+// the 256-CU MI355X), which is full occupancy for this register budget; work is per-pair
+// independent, so no LDS, no atomics and no inter-workgroup traffic are needed.  Parameters are
+// passed by value in the kernarg segment and stay in SGPRs.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/bbm_hip.h"
+#include "diffuse.hpp"
+#include "math.hpp"
+#include "microfacet.hpp"
+
+namespace bbmhip {
+namespace {
+
+constexpr int kMaxParams = 64;
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = 256 * 8;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+  g_last_error = msg;
+  return code;
+}
+
+struct ParamBlock { float v[kMaxParams]; };
+
+struct EvalArgs
+{
+  const float* ix; const float* iy; const float* iz;
+  const float* ox; const float* oy; const float* oz;
+  const uint8_t* mask;
+  float* r; float* g; float* b; float* pdf;
+  uint64_t n;
+  uint32_t component;
+  ParamBlock p;
+};
+
+template<class Model, int MODE>
+__device__ __forceinline__ void one_pair(const Model& m, const EvalArgs& a, uint64_t i, bool active)
+{
+  float rgb[3], pdf;
+  const v3 in = mk3(a.ix[i], a.iy[i], a.iz[i]);
+  const v3 out = mk3(a.ox[i], a.oy[i], a.oz[i]);
+  m.template eval_pdf<MODE>(in, out, active ? a.component : 0u, rgb, pdf);
+  if (MODE & kModeEval) { a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2]; }
+  if (MODE & kModePdf) a.pdf[i] = pdf;
+}
+
+// Vector path: 4 consecutive pairs per thread-iteration, 16-byte loads/stores per array.
+// Requires every array 16-byte aligned (checked on the host); the n % 4 tail runs scalar.
+template<class Model, int MODE, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
+  {
+    const float4 ix = reinterpret_cast<const float4*>(a.ix)[t];
+    const float4 iy = reinterpret_cast<const float4*>(a.iy)[t];
+    const float4 iz = reinterpret_cast<const float4*>(a.iz)[t];
+    const float4 ox = reinterpret_cast<const float4*>(a.ox)[t];
+    const float4 oy = reinterpret_cast<const float4*>(a.oy)[t];
+    const float4 oz = reinterpret_cast<const float4*>(a.oz)[t];
+    uint32_t mk = 0x01010101u;
+    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
+    const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
+    float r[4], g[4], b[4], p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      float rgb[3];
+      const uint32_t comp = ((mk >> (8 * j)) & 0xffu) ? a.component : 0u;
+      m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
+      r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
+    }
+    if (MODE & kModeEval)
+    {
+      reinterpret_cast<float4*>(a.r)[t] = make_float4(r[0], r[1], r[2], r[3]);
+      reinterpret_cast<float4*>(a.g)[t] = make_float4(g[0], g[1], g[2], g[3]);
+      reinterpret_cast<float4*>(a.b)[t] = make_float4(b[0], b[1], b[2], b[3]);
+    }
+    if (MODE & kModePdf) reinterpret_cast<float4*>(a.pdf)[t] = make_float4(p[0], p[1], p[2], p[3]);
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+// Scalar path for unaligned arrays.
+template<class Model, int MODE, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template<class Model, int MODE, bool MASK>
+int launch_mode(const EvalArgs& a, hipStream_t s)
+{
+  bool vec = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
+             aligned16(a.oz) && (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
+  if (MODE & kModeEval) vec = vec && aligned16(a.r) && aligned16(a.g) && aligned16(a.b);
+  if (MODE & kModePdf) vec = vec && aligned16(a.pdf);
+  const uint64_t units = vec ? (a.n >> 2) : a.n;
+  uint64_t blocks = (units + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+template<class Model>
+int launch_eval_pdf(const EvalArgs& a, int mode, hipStream_t s)
+{
+  const bool mk = a.mask != nullptr;
+  switch (mode)
+  {
+    case kModeEval: return mk ? launch_mode<Model, kModeEval, true>(a, s) : launch_mode<Model, kModeEval, false>(a, s);
+    case kModePdf: return mk ? launch_mode<Model, kModePdf, true>(a, s) : launch_mode<Model, kModePdf, false>(a, s);
+    default: return mk ? launch_mode<Model, kModeEvalPdf, true>(a, s) : launch_mode<Model, kModeEvalPdf, false>(a, s);
+  }
+}
+
+// ------------------------------------------------------------------------ model registry
+
+using EvalLauncher = int (*)(const EvalArgs&, int, hipStream_t);
+
+struct ModelEntry
+{
+  const char* name;
+  int nparams;
+  uint32_t components;
+  EvalLauncher eval_pdf;
+  float defaults[kMaxParams];
+  float lower[kMaxParams];
+  float upper[kMaxParams];
+};
+
+// Compositions (reference file:line):
+using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;         // bsdfmodel/cooktorrance.h:28-34
+using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                        // bsdfmodel/ggx.h:27-33
+using CookTorranceWalterM = Microfacet<Beckmann<false, true>, Uncorrelated, FresnelCook, Norm::Walter, true>;  // bsdfmodel/cooktorrancewalter.h:32-38
+
+constexpr float kFMax = 3.4028234663852886e+38f;
+
+// Defaults and bounds: bsdf_attribute.h:73-94 (scale 0.5 in [0,1], roughness 0.1 in [0,1] as
+// reported by parameter_lower_bound/upper_bound, ior 1.3 in [1,5]); pinned against
+// tests/golden/models.json by tests/test_abi.py.
+const ModelEntry kModels[] = {
+  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>,
+   {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}},
+  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,   // bsdfmodel/low.h:32-33
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+};
+constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
+
+const ModelEntry* entry(int id) { return (id >= 0 && id < kNumModels) ? &kModels[id] : nullptr; }
+
+int prepare(int model_id, const float* params, int nparams, size_t n, EvalArgs& a, const ModelEntry*& e)
+{
+  e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  if (nparams != e->nparams)
+    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
+                                             " parameters, got " + std::to_string(nparams));
+  if (nparams > 0 && !params) return fail(BBM_HIP_ERR_INVALID_ARG, "params is NULL");
+  std::memset(&a, 0, sizeof(a));
+  for (int i = 0; i < nparams; ++i) a.p.v[i] = params[i];
+  a.n = n;
+  return BBM_HIP_OK;
+}
+
+int check_dirs(const float* x, const float* y, const float* z, const char* what)
+{
+  if (!x || !y || !z) return fail(BBM_HIP_ERR_INVALID_ARG, std::string(what) + " direction pointer is NULL");
+  return BBM_HIP_OK;
+}
+
+// ------------------------------------------------------------------- synthetic directions
+
+// Counter-based generator: splitmix64 finaliser over (seed, stream, index).  Two 24-bit uniforms
+// per direction.  Pure function of the global index -> shards regenerate identical slices.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_dirs(uint64_t key, uint64_t offset, uint64_t n, int mode,
+                                                       float* __restrict__ x, float* __restrict__ y, float* __restrict__ z)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+  {
+    const uint64_t h = mix64(key + 0x9e3779b97f4a7c15ull * (offset + i));
+    const float u1 = float(uint32_t(h >> 40)) * (1.0f / 16777216.0f);
+    const float u2 = float(uint32_t(h >> 16) & 0xffffffu) * (1.0f / 16777216.0f);
+    const float zz = (mode == 0) ? u1 : 2.0f * u1 - 1.0f;
+    const float s = sqrtf(fmaxf(1.0f - zz * zz, 0.0f));
+    float sp, cp;
+    sincosf(2.0f * kPiF * u2, &sp, &cp);
+    x[i] = s * cp;
+    y[i] = s * sp;
+    z[i] = zz;
+  }
+}
+
+}  // namespace
+}  // namespace bbmhip
+
+using namespace bbmhip;
+
+extern "C" {
+
+int bbm_hip_abi_version(void) { return BBM_HIP_ABI_VERSION; }
+
+const char* bbm_hip_last_error(void) { return g_last_error.c_str(); }
+
+int bbm_hip_num_models(void) { return kNumModels; }
+
+const char* bbm_hip_model_name(int model_id)
+{
+  const ModelEntry* e = entry(model_id);
+  return e ? e->name : nullptr;
+}
+
+int bbm_hip_model_id(const char* name)
+{
+  if (!name) return fail(BBM_HIP_ERR_INVALID_ARG, "name is NULL");
+  for (int i = 0; i < kNumModels; ++i)
+    if (std::strcmp(kModels[i].name, name) == 0) return i;
+  return fail(BBM_HIP_ERR_INVALID_MODEL, std::string("unknown BSDF model: ") + name);
+}
+
+int bbm_hip_model_nparams(int model_id)
+{
+  const ModelEntry* e = entry(model_id);
+  return e ? e->nparams : fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+}
+
+int bbm_hip_model_params(int model_id, int which, float* out, int capacity)
+{
+  const ModelEntry* e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  const float* src = (which == 0) ? e->defaults : (which == 1) ? e->lower : (which == 2) ? e->upper : nullptr;
+  if (!src) return fail(BBM_HIP_ERR_INVALID_ARG, "which must be 0 (default), 1 (lower) or 2 (upper)");
+  for (int i = 0; out && i < e->nparams && i < capacity; ++i) out[i] = src[i];
+  return e->nparams;
+}
+
+int bbm_hip_model_components(int model_id)
+{
+  const ModelEntry* e = entry(model_id);
+  return e ? int(e->components) : fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+}
+
+static int eval_common(int mode, int model_id, const float* params, int nparams,
+                       const float* in_x, const float* in_y, const float* in_z,
+                       const float* out_x, const float* out_y, const float* out_z,
+                       const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                       float* r, float* g, float* b, float* pdf, void* stream)
+{
+  (void)unit;   // no model on this path depends on unit_t (bsdfmodel/microfacet.h:74, lambertian.h:45)
+  EvalArgs a;
+  const ModelEntry* e;
+  int rc = prepare(model_id, params, nparams, n, a, e);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if ((rc = check_dirs(in_x, in_y, in_z, "in")) || (rc = check_dirs(out_x, out_y, out_z, "out"))) return rc;
+  if ((mode & kModeEval) && (!r || !g || !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "eval output pointer is NULL");
+  if ((mode & kModePdf) && !pdf) return fail(BBM_HIP_ERR_INVALID_ARG, "pdf output pointer is NULL");
+  a.ix = in_x; a.iy = in_y; a.iz = in_z; a.ox = out_x; a.oy = out_y; a.oz = out_z;
+  a.mask = mask; a.r = r; a.g = g; a.b = b; a.pdf = pdf;
+  a.component = component & kFlagAll;
+  return e->eval_pdf(a, mode, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_eval(int model_id, const float* params, int nparams,
+                 const float* in_x, const float* in_y, const float* in_z,
+                 const float* out_x, const float* out_y, const float* out_z,
+                 const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                 float* r, float* g, float* b, void* stream)
+{
+  return eval_common(kModeEval, model_id, params, nparams, in_x, in_y, in_z, out_x, out_y, out_z, mask, n,
+                     component, unit, r, g, b, nullptr, stream);
+}
+
+int bbm_hip_pdf(int model_id, const float* params, int nparams,
+                const float* in_x, const float* in_y, const float* in_z,
+                const float* out_x, const float* out_y, const float* out_z,
+                const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                float* pdf, void* stream)
+{
+  return eval_common(kModePdf, model_id, params, nparams, in_x, in_y, in_z, out_x, out_y, out_z, mask, n,
+                     component, unit, nullptr, nullptr, nullptr, pdf, stream);
+}
+
+int bbm_hip_eval_pdf(int model_id, const float* params, int nparams,
+                     const float* in_x, const float* in_y, const float* in_z,
+                     const float* out_x, const float* out_y, const float* out_z,
+                     const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                     float* r, float* g, float* b, float* pdf, void* stream)
+{
+  return eval_common(kModeEvalPdf, model_id, params, nparams, in_x, in_y, in_z, out_x, out_y, out_z, mask, n,
+                     component, unit, r, g, b, pdf, stream);
+}
+
+int bbm_hip_sample(int model_id, const float* params, int nparams,
+                   const float* out_x, const float* out_y, const float* out_z,
+                   const float* xi0, const float* xi1,
+                   const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                   float* dir_x, float* dir_y, float* dir_z, float* pdf, uint32_t* flag,
+                   void* stream)
+{
+  (void)params; (void)nparams; (void)out_x; (void)out_y; (void)out_z; (void)xi0; (void)xi1; (void)mask;
+  (void)n; (void)component; (void)unit; (void)dir_x; (void)dir_y; (void)dir_z; (void)pdf; (void)flag; (void)stream;
+  if (!entry(model_id)) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  return fail(BBM_HIP_ERR_UNSUPPORTED, "sample is not implemented yet for this model");
+}
+
+int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,
+                            float* x, float* y, float* z, void* stream)
+{
+  if (n == 0) return BBM_HIP_OK;
+  if (!x || !y || !z) return fail(BBM_HIP_ERR_INVALID_ARG, "direction pointer is NULL");
+  if (mode != 0 && mode != 1) return fail(BBM_HIP_ERR_INVALID_ARG, "mode must be 0 (hemisphere) or 1 (sphere)");
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  const uint64_t key = mix64(seed) ^ (0xd1b54a32d192ed03ull * (uint64_t(stream_id) + 1));
+  hipLaunchKernelGGL(k_fill_dirs, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), key,
+                     offset, uint64_t(n), mode, x, y, z);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// bbm_amd/csrc/math.hpp -- device math layer of the HIP backbone.
+//
+// The BBM native backbone (backbone/native/include/backbone/{math,horizontal,array}.h) fixes the
+// rounding of every intermediate: Value = float, but C++'s usual arithmetic conversions promote
+// a handful of intermediates to double (`2.0 * x`, `x / literal<double>`, `bbm::max(x, 0.0)`,
+// `bbm::pow(x, 2.0)`).  HIP device code obeys the same conversions, so the model code in this
+// directory keeps the reference's literal types and lets the compiler do the same promotions;
+// the few helpers here pin down the ones that are library behaviour rather than language rules.
+// The whole TU is compiled with -ffp-contract=off: every float op rounds on its own, exactly as
+// the reference's x86-64 build does, so results match the CPU backbone to ~1 ulp (transcendentals
+// are the only non-correctly-rounded ops on either side).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bbmhip {
+
+// bsdf_flag (include/bbm/bsdf_flag.h:21-27), unit_t (include/bbm/unit.h:20-24)
+enum : uint32_t { kFlagNone = 0, kFlagDiffuse = 1, kFlagSpecular = 2, kFlagAll = 3 };
+
+constexpr double kPiD = 3.141592653589793238462643383279502884;
+constexpr double kInvPiD = 0.318309886183790671537767526745028724;
+constexpr double kInvSqrtPiD = 0.564189583547756286948079451560772586;
+// constants<float>::Pi()/InvPi() (include/core/constants.h:17-19) = T(scale * std::numbers::pi)
+constexpr float kPiF = float(1.0f * kPiD);
+constexpr float kInvPiF = float(1.0f * kInvPiD);
+constexpr float kInvSqrtPiF = float(1.0f * kInvSqrtPiD);
+constexpr float kEpsF = 1.1920928955078125e-07f;   // numeric_limits<float>::epsilon()
+
+struct v3 { float x, y, z; };
+struct v2 { float x, y; };
+
+__device__ __forceinline__ v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
+
+// horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2
+__device__ __forceinline__ float dot3(v3 a, v3 b) { return ((0.0f + a.x * b.x) + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ float sqnorm2(float a, float b) { return (0.0f + a * a) + b * b; }
+
+// horizontal.h:96-100 normalize = t * rsqrt(|t|^2); math.h:109-112 rsqrt = rcp(sqrt) = 1 / sqrt
+__device__ __forceinline__ v3 normalize3(v3 t)
+{
+  const float r = 1 / sqrtf(dot3(t, t));
+  return mk3(t.x * r, t.y * r, t.z * r);
+}
+
+// core/vec_transform.h:76-80
+__device__ __forceinline__ v3 halfway(v3 a, v3 b) { return normalize3(mk3(a.x + b.x, a.y + b.y, a.z + b.z)); }
+
+// core/vec_transform.h:58-64 cross
+__device__ __forceinline__ v3 cross3(v3 a, v3 b)
+{
+  return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+// math.h:129 safe_sqrt = sqrt(std::max(a, T(0))): std::max keeps a NaN argument (a < 0 is false)
+__device__ __forceinline__ float safe_sqrtf(float a) { return sqrtf((a < 0.0f) ? 0.0f : a); }
+__device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
+
+// core/spherical.h:79-80 sinTheta2 = bbm::max(1 - z*z, 0) -> fmaxf (result_t<float,int> = float)
+__device__ __forceinline__ float sin_theta2(v3 v) { return fmaxf(1 - v.z * v.z, 0.0f); }
+// spherical.h:179-180 tanTheta = sinTheta / cosTheta; :185-186 tanTheta2 = sinTheta2 / cosTheta2
+__device__ __forceinline__ float tan_theta(v3 v) { return sqrtf(sin_theta2(v)) / v.z; }
+__device__ __forceinline__ float tan_theta2(v3 v) { return sin_theta2(v) / (v.z * v.z); }
+
+// bbm::pow(float, int) -> std::pow(float, float); for the exponent 2 used on this path the
+// correctly rounded square is what glibc's powf returns.
+__device__ __forceinline__ float pow2f(float x) { return x * x; }
+
+}  // namespace bbmhip

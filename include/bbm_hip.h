@@ -1,0 +1,122 @@
+/* include/bbm_hip.h -- C-ABI of libbbm_hip.so, the MI355X (gfx950) batched BSDF backbone.
+ *
+ * This is the drop-in boundary for BBM's hot path.  In the reference, a bsdfmodel<> is evaluated
+ * one (in, out) pair per call through the template API of the bsdfmodel concept
+ * (include/concepts/bsdfmodel.h:33-146):
+ *
+ *   Spectrum   eval(const Vec3d& in, const Vec3d& out, BsdfFlag component, unit_t unit, Mask mask)
+ *   Value      pdf(const Vec3d& in, const Vec3d& out, BsdfFlag component, unit_t unit, Mask mask)
+ *   BsdfSample sample(const Vec3d& out, const Vec2d& xi, BsdfFlag component, unit_t unit, Mask mask)
+ *   Spectrum   reflectance(const Vec3d& out, BsdfFlag component, unit_t unit, Mask mask)
+ *
+ * and batching only exists when the backbone's Value is a wide type (backbone/enoki,
+ * backbone/drjit).  Here the same four calls take N pairs at once: directions are SoA float32
+ * device arrays (x[], y[], z[]), the per-lane Mask is an optional uint8 array, and `component` /
+ * `unit` are uniform per call.  Model parameters are the flat bbm::parameter_values() vector
+ * (include/bbm/bsdf_enumerate.h; attribute declaration order, Dependent attributes included),
+ * uniform per call.  All pointers are caller-owned device memory; calls are asynchronous on
+ * `stream` (a hipStream_t; NULL = the default stream) and never synchronise.
+ *
+ * Errors: the reference throws C++ exceptions (include/core/error.h:42-46); here every entry
+ * point returns BBM_HIP_OK (0) or a negative code and records a message readable through
+ * bbm_hip_last_error() (thread-local).  No exception crosses this ABI.
+ */
+#ifndef BBM_HIP_H
+#define BBM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BBM_HIP_ABI_VERSION 1
+
+/* return codes */
+#define BBM_HIP_OK 0
+#define BBM_HIP_ERR_INVALID_MODEL -1   /* unknown model id / name (reference: std::invalid_argument, bsdf_string_convert.h:70-75) */
+#define BBM_HIP_ERR_INVALID_ARG -2     /* null pointer, bad parameter count, ... */
+#define BBM_HIP_ERR_UNSUPPORTED -3     /* operation not (yet) available for this model */
+#define BBM_HIP_ERR_HIP -4             /* HIP runtime error (launch failure) */
+
+/* bsdf_flag (include/bbm/bsdf_flag.h:21-27) */
+#define BBM_FLAG_NONE 0u
+#define BBM_FLAG_DIFFUSE 1u
+#define BBM_FLAG_SPECULAR 2u
+#define BBM_FLAG_ALL 3u
+
+/* unit_t (include/bbm/unit.h:20-24) */
+#define BBM_UNIT_RADIANCE 0u
+#define BBM_UNIT_IMPORTANCE 1u
+
+/* ---------------------------------------------------------------- library / registry */
+
+/* ABI version of the loaded library (BBM_HIP_ABI_VERSION). */
+int bbm_hip_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* bbm_hip_last_error(void);
+
+/* Model registry.  Replaces the compile-time registry of BBM_EXPORT_BSDFMODEL
+ * (e.g. include/bsdfmodel/cooktorrance.h:42) and the keyword lookup of
+ * fromString<bsdf_ptr> (include/bbm/bsdf_string_convert.h:52-82). */
+int bbm_hip_num_models(void);
+const char* bbm_hip_model_name(int model_id);          /* NULL if out of range */
+int bbm_hip_model_id(const char* name);                 /* <0 if unknown */
+int bbm_hip_model_nparams(int model_id);                /* length of the parameter vector */
+/* Default / lower / upper parameter vectors (bsdf_attribute.h defaults and bounds;
+ * bbm::parameter_default_values / parameter_lower_bound / parameter_upper_bound,
+ * include/bbm/bsdf_enumerate.h).  which: 0 = default, 1 = lower, 2 = upper.  Returns nparams. */
+int bbm_hip_model_params(int model_id, int which, float* out, int capacity);
+/* Component flags the model can return non-zero values for (BBM_FLAG_*). */
+int bbm_hip_model_components(int model_id);
+
+/* ---------------------------------------------------------------- batched evaluation */
+
+/* eval (RGB Spectrum) for n pairs -- bsdfmodel::eval, e.g. bsdfmodel/microfacet.h:74-102. */
+int bbm_hip_eval(int model_id, const float* params, int nparams,
+                 const float* in_x, const float* in_y, const float* in_z,
+                 const float* out_x, const float* out_y, const float* out_z,
+                 const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                 float* r, float* g, float* b, void* stream);
+
+/* pdf for n pairs -- bsdfmodel::pdf, e.g. bsdfmodel/microfacet.h:154-174. */
+int bbm_hip_pdf(int model_id, const float* params, int nparams,
+                const float* in_x, const float* in_y, const float* in_z,
+                const float* out_x, const float* out_y, const float* out_z,
+                const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                float* pdf, void* stream);
+
+/* Fused eval + pdf over the same pairs (one read of the directions, one kernel): the headline
+ * path (BASELINE.json metric).  Results are identical to bbm_hip_eval + bbm_hip_pdf. */
+int bbm_hip_eval_pdf(int model_id, const float* params, int nparams,
+                     const float* in_x, const float* in_y, const float* in_z,
+                     const float* out_x, const float* out_y, const float* out_z,
+                     const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                     float* r, float* g, float* b, float* pdf, void* stream);
+
+/* sample (direction, pdf, flag) for n (out, xi) -- bsdfmodel::sample, e.g. microfacet.h:115-141.
+ * flag receives the bsdf_flag of each sample (BBM_FLAG_*). */
+int bbm_hip_sample(int model_id, const float* params, int nparams,
+                   const float* out_x, const float* out_y, const float* out_z,
+                   const float* xi0, const float* xi1,
+                   const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                   float* dir_x, float* dir_y, float* dir_z, float* pdf, uint32_t* flag,
+                   void* stream);
+
+/* ---------------------------------------------------------------- synthetic directions */
+
+/* Fill n directions from a counter-based generator: element i depends only on (seed, offset + i),
+ * so shards on different GPUs regenerate their slice of one global batch without any scatter.
+ * mode 0: uniform in z on the upper hemisphere (z = u, phi = 2 pi u'), the worst case with every
+ * lane active; mode 1: uniform on the sphere (bin/checkBsdf.cpp:28-35 sampleSphere).
+ * stream_id selects an independent stream of the generator (e.g. 0 = in, 1 = out). */
+int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,
+                            float* x, float* y, float* z, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BBM_HIP_H */

@@ -1,0 +1,299 @@
+/* oracle/port/bbm_port.c -- TEST INFRASTRUCTURE ONLY (see bbm_port.h).
+ *
+ * Plain-C restatement of the BBM native backbone (floatRGB) for the batched eval/pdf/sample path.
+ * Every function cites the reference file:line it restates.  Precision follows the native
+ * backbone exactly: Value = float, but C++ promotion makes some intermediates double -- e.g.
+ * `2.0 * z * z / dot` (maskingshadowing/vgroove.h:41-43), `x / NormalizationFactor` with a
+ * literal<double> (bsdfmodel/microfacet.h:100), `bbm::max(x, 0.0)` (backbone/native/include/
+ * backbone/math.h:100-103 result_t promotion).  C has the same usual arithmetic conversions, so
+ * each expression below keeps the reference's literal types; contraction is disabled at build
+ * time (-ffp-contract=off) so every float op is rounded on its own, like the reference build.
+ */
+#include "bbm_port.h"
+
+#include <math.h>
+#include <string.h>
+
+#define PI_D 3.141592653589793238462643383279502884
+#define INV_PI_D 0.318309886183790671537767526745028724
+
+/* bsdf_flag (include/bbm/bsdf_flag.h:21-27) */
+enum { FLAG_NONE = 0, FLAG_DIFFUSE = 1, FLAG_SPECULAR = 2, FLAG_ALL = 3 };
+
+typedef struct { float x, y, z; } v3;
+
+/* constants<float> (include/core/constants.h:17-23): T(scale * double constant) */
+static const float kPiF = (float)(1.0f * PI_D);
+static const float kInvPiF = (float)(1.0f * INV_PI_D);
+
+/* backbone/native/include/backbone/horizontal.h:78-82 dot = inner_product(..., T(0)) */
+static inline float dot3(v3 a, v3 b) { return ((0.0f + a.x * b.x) + a.y * b.y) + a.z * b.z; }
+
+/* horizontal.h:96-100 normalize = t * rsqrt(squared_norm(t)); math.h:109-112 rsqrt = 1/sqrt */
+static inline v3 normalize3(v3 t)
+{
+  float r = 1 / sqrtf(dot3(t, t));
+  v3 o = { t.x * r, t.y * r, t.z * r };
+  return o;
+}
+
+/* core/vec_transform.h:76-80 halfway = normalize(a + b) */
+static inline v3 halfway(v3 a, v3 b)
+{
+  v3 t = { a.x + b.x, a.y + b.y, a.z + b.z };
+  return normalize3(t);
+}
+
+/* std::max(a, T(0)) semantics (NaN passes through), math.h:129 safe_sqrt */
+static inline float safe_sqrtf(float a) { return sqrtf((a < 0.0f) ? 0.0f : a); }
+static inline double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
+
+/* core/spherical.h:79-80 sinTheta2 = max(1 - z*z, 0) (float fmax); :179-180 tanTheta = sinT / cosT */
+static inline float sin_theta2(v3 v) { return fmaxf(1 - v.z * v.z, 0); }
+static inline float tan_theta(v3 v) { return sqrtf(sin_theta2(v)) / v.z; }
+static inline float tan_theta2(v3 v) { return sin_theta2(v) / (v.z * v.z); }
+
+/* ---------------------------------------------------------------- NDFs */
+
+/* ndf/beckmann.h:49-66 eval */
+static float beckmann_eval(v3 h, float au, float av, int normalize)
+{
+  if (!(h.z > 0)) return 0;
+  float c2 = h.z * h.z;
+  float sx = h.x / au, sy = h.y / av;
+  float sn = (0.0f + sx * sx) + sy * sy;
+  float D = expf(-sn / c2) / (au * av * c2 * c2);
+  if (normalize) D *= kInvPiF;
+  return D;
+}
+
+/* ndf/beckmann.h:180-201 G1 (isotropic branch `rcp(roughness * tanTheta(v))`; the anisotropic
+   branch `rsqrt(|xy*roughness|^2 / pow(z,2))`) */
+static float beckmann_G1(v3 v, v3 m, float au, float av, int aniso)
+{
+  if (!((v.z > 0) && (dot3(v, m) > 0))) return 0;
+  float a;
+  if (aniso)
+  {
+    float px = v.x * au, py = v.y * av;
+    float sn = (0.0f + px * px) + py * py;
+    a = 1 / sqrtf(sn / powf(v.z, 2.0f));
+  }
+  else a = 1 / (au * tan_theta(v));
+  double g = (a < 1.6) ? (3.535 * a + 2.181 * a * a) / (1 + 2.276 * a + 2.577 * a * a) : 1.0;
+  return (float)g;
+}
+
+/* ndf/ggx.h:50-65 eval */
+static float ggx_eval(v3 h, float au, float av)
+{
+  if (!(h.z > 0)) return 0;
+  float alpha2 = (1.0f * au) * av;            /* hprod, horizontal.h:64-68 */
+  float sx = h.x / au, sy = h.y / av;
+  float sn = (0.0f + sx * sx) + sy * sy;
+  double d = kPiF * alpha2 * pow((double)(sn + powf(h.z, 2.0f)), 2.0);
+  return (float)(1 / d);
+}
+
+/* ndf/ggx.h:173-189 G1 */
+static float ggx_G1(v3 v, v3 m, float au, float av)
+{
+  if (!((v.z > 0) && (dot3(v, m) > 0))) return 0;
+  float r2 = (1.0f * au) * av;
+  float t2 = tan_theta2(v);
+  float denom = (float)(1.0 + sqrt(1.0 + r2 * t2));
+  return (float)(2.0 / denom);
+}
+
+/* ndf/{beckmann,ggx}.h pdf (beckmann.h:149-170, ggx.h:142-163): VNDF pdf D*G1*|v.m|/cos(v) */
+typedef enum { NDF_BECKMANN, NDF_BECKMANN_NORM, NDF_GGX } ndf_kind;
+
+static float ndf_eval(ndf_kind k, v3 h, float au, float av)
+{
+  return (k == NDF_GGX) ? ggx_eval(h, au, av) : beckmann_eval(h, au, av, k == NDF_BECKMANN_NORM);
+}
+
+static float ndf_G1(ndf_kind k, v3 v, v3 m, float au, float av, int aniso)
+{
+  return (k == NDF_GGX) ? ggx_G1(v, m, au, av) : beckmann_G1(v, m, au, av, aniso);
+}
+
+static float ndf_pdf(ndf_kind k, v3 view, v3 m, float au, float av, int aniso)
+{
+  if (!(m.z > 0)) return 0;
+  float pdf = ndf_eval(k, m, au, av);
+  pdf *= ndf_G1(k, view, m, au, av, aniso) * fabsf(dot3(view, m)) / view.z;
+  if (!(pdf > 0)) return 0;
+  return pdf;
+}
+
+/* ---------------------------------------------------------------- masking-shadowing */
+
+typedef enum { MS_VGROOVE, MS_UNCORRELATED } ms_kind;
+
+/* maskingshadowing/vgroove.h:30-47 (double via 2.0 literal, fmin) and uncorrelated.h:30-42 */
+static float ms_eval(ms_kind ms, ndf_kind k, v3 in, v3 out, v3 m, float au, float av, int aniso)
+{
+  if (!((dot3(in, m) > 0) && (dot3(out, m) > 0))) return 0;
+  if (ms == MS_VGROOVE)
+  {
+    double gi = 2.0 * m.z * in.z / dot3(in, m);
+    double go = 2.0 * m.z * out.z / dot3(out, m);
+    return (float)fmin(1.0, fmin(gi, go));
+  }
+  return ndf_G1(k, in, m, au, av, aniso) * ndf_G1(k, out, m, au, av, aniso);
+}
+
+/* ---------------------------------------------------------------- fresnel */
+
+/* bbm/fresnel_cook.h:41-56 (float math; final bbm::max(x, 0.0) in double -> NaN becomes 0) */
+static float fresnel_cook(float eta, float c)
+{
+  float g = safe_sqrtf(eta * eta + c * c - 1.0f);
+  float a = (g - c) / (g + c);
+  float b = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
+  return (float)fmax(0.5f * (a * a) * (1.0f + b * b), 0.0);
+}
+
+/* ---------------------------------------------------------------- models */
+
+typedef struct {
+  const char* name;
+  ndf_kind ndf;
+  ms_kind ms;
+  double norm;       /* microfacet_n (bsdfmodel/microfacet.h:31-36) */
+  int aniso;         /* roughness is a Vec2d */
+} microfacet_desc;
+
+/* composition table: bsdfmodel/cooktorrance.h:28-34, ggx.h:27-33, cooktorrancewalter.h:32-38,
+   low.h:32-33 (LowCookTorrance == cooktorrance) */
+static const microfacet_desc kMicrofacet[] = {
+  { "CookTorrance",       NDF_BECKMANN,      MS_VGROOVE,      PI_D, 0 },
+  { "LowCookTorrance",    NDF_BECKMANN,      MS_VGROOVE,      PI_D, 0 },
+  { "GGX",                NDF_GGX,           MS_UNCORRELATED, 4.0,  0 },
+  { "CookTorranceWalter", NDF_BECKMANN_NORM, MS_UNCORRELATED, 4.0,  0 },
+};
+#define N_MICROFACET (int)(sizeof(kMicrofacet) / sizeof(kMicrofacet[0]))
+
+/* bsdfmodel/microfacet.h:74-102 eval (scaled by albedo in scaledmodel.h:50-53) */
+static void microfacet_eval(const microfacet_desc* d, const float* p, v3 in, v3 out, uint32_t comp, float* rgb)
+{
+  rgb[0] = rgb[1] = rgb[2] = 0;
+  if (!(comp & FLAG_SPECULAR)) return;
+  if (!((in.z > 0.0f) && (out.z > 0.0f))) return;
+  const float au = p[3], av = d->aniso ? p[4] : p[3], eta = d->aniso ? p[5] : p[4];
+  v3 h = halfway(in, out);
+  float inh = dot3(in, h), outh = dot3(out, h);
+  float D = ndf_eval(d->ndf, h, au, av);
+  float G = ms_eval(d->ms, d->ndf, in, out, h, au, av, d->aniso);
+  float F = fresnel_cook(eta, 0.5f * (inh + outh));
+  float res = (float)(D * G * F / d->norm / (in.z * out.z));
+  rgb[0] = res * p[0]; rgb[1] = res * p[1]; rgb[2] = res * p[2];
+}
+
+/* bsdfmodel/microfacet.h:154-174 pdf */
+static float microfacet_pdf(const microfacet_desc* d, const float* p, v3 in, v3 out, uint32_t comp)
+{
+  if (!(comp & FLAG_SPECULAR)) return 0;
+  if (!((out.z > 0) && (in.z > 0))) return 0;
+  const float au = p[3], av = d->aniso ? p[4] : p[3];
+  v3 h = halfway(in, out);
+  if (h.z < 0) { h.x = -h.x; h.y = -h.y; h.z = -h.z; }
+  double pdf = ndf_pdf(d->ndf, out, h, au, av, d->aniso) / (4.0 * fabsf(dot3(out, h)));
+  return (float)pdf;
+}
+
+/* bsdfmodel/lambertian.h:45-59 eval, 115-125 pdf (non-strict z >= 0) */
+static void lambertian_eval(const float* p, v3 in, v3 out, uint32_t comp, float* rgb)
+{
+  rgb[0] = rgb[1] = rgb[2] = 0;
+  if (!(comp & FLAG_DIFFUSE)) return;
+  if (!((in.z >= 0) && (out.z >= 0))) return;
+  rgb[0] = p[0] * kInvPiF; rgb[1] = p[1] * kInvPiF; rgb[2] = p[2] * kInvPiF;
+}
+
+static float lambertian_pdf(v3 in, v3 out, uint32_t comp)
+{
+  if (!(comp & FLAG_DIFFUSE)) return 0;
+  if (!((in.z >= 0) && (out.z >= 0))) return 0;
+  return in.z * kInvPiF;
+}
+
+/* bsdfmodel/lambertian.h:76-103 sample (cosine-weighted) */
+static void lambertian_sample(v3 out, float xi0, float xi1, uint32_t comp, v3* dir, float* pdf, uint32_t* flag)
+{
+  dir->x = dir->y = dir->z = 0; *pdf = 0; *flag = FLAG_NONE;
+  if (!(comp & FLAG_DIFFUSE)) return;
+  if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+  float phi = xi0 * (float)(2.0f * PI_D);                  /* Constants::Pi(2) */
+  float c = cosf(phi), s = sinf(phi);
+  float sin_t = (float)safe_sqrt(1.0 - xi1);
+  dir->x = c * sin_t; dir->y = s * sin_t; dir->z = safe_sqrtf(xi1);
+  *pdf = lambertian_pdf(*dir, out, comp);
+  *flag = FLAG_DIFFUSE;
+}
+
+/* ---------------------------------------------------------------- dispatch */
+
+enum { M_LAMBERTIAN = -1 };
+
+static int find_model(const char* name)
+{
+  if (strcmp(name, "Lambertian") == 0) return M_LAMBERTIAN;
+  for (int i = 0; i < N_MICROFACET; ++i)
+    if (strcmp(name, kMicrofacet[i].name) == 0) return i;
+  return -1000;
+}
+
+int bbmport_num_models(void) { return N_MICROFACET + 1; }
+
+const char* bbmport_model_name(int i)
+{
+  if (i == 0) return "Lambertian";
+  if (i >= 1 && i <= N_MICROFACET) return kMicrofacet[i - 1].name;
+  return 0;
+}
+
+int bbmport_eval_pdf(const char* name, const float* params, int nparams, size_t n,
+                     const float* ix, const float* iy, const float* iz,
+                     const float* ox, const float* oy, const float* oz,
+                     uint32_t component, uint32_t unit, int mode,
+                     float* r, float* g, float* b, float* pdf, int nthreads)
+{
+  (void)unit; (void)nparams;   /* unit is ignored by every model on this path */
+  int m = find_model(name);
+  if (m == -1000) return -1;
+  const microfacet_desc* d = (m >= 0) ? &kMicrofacet[m] : 0;
+  #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+  for (long long i = 0; i < (long long)n; ++i)
+  {
+    v3 in = { ix[i], iy[i], iz[i] }, out = { ox[i], oy[i], oz[i] };
+    if (mode & 1)
+    {
+      float rgb[3];
+      if (d) microfacet_eval(d, params, in, out, component, rgb);
+      else lambertian_eval(params, in, out, component, rgb);
+      r[i] = rgb[0]; g[i] = rgb[1]; b[i] = rgb[2];
+    }
+    if (mode & 2) pdf[i] = d ? microfacet_pdf(d, params, in, out, component) : lambertian_pdf(in, out, component);
+  }
+  return 0;
+}
+
+int bbmport_sample(const char* name, const float* params, int nparams, size_t n,
+                   const float* ox, const float* oy, const float* oz,
+                   const float* xi0, const float* xi1, uint32_t component, uint32_t unit,
+                   float* dx, float* dy, float* dz, float* pdf, uint32_t* flag, int nthreads)
+{
+  (void)unit; (void)nparams; (void)params;
+  int m = find_model(name);
+  if (m != M_LAMBERTIAN) return -2;   /* microfacet sampling: see DESIGN.md (next row) */
+  #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+  for (long long i = 0; i < (long long)n; ++i)
+  {
+    v3 out = { ox[i], oy[i], oz[i] }, dir;
+    lambertian_sample(out, xi0[i], xi1[i], component, &dir, &pdf[i], &flag[i]);
+    dx[i] = dir.x; dy[i] = dir.y; dz[i] = dir.z;
+  }
+  return 0;
+}

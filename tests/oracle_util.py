@@ -1,0 +1,175 @@
+"""Test-side access to the oracle (CPU checkers) and the golden fixtures.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+  * port: oracle/_port/libbbm_port.so -- our C restatement of the native backbone (oracle/port);
+  * ref : oracle/_ref/libbbm_ref.so   -- the reference's own headers behind a ctypes shim
+          (prebuilt in the build container; absent if it was never built);
+  * golden: tests/golden/*.npz written by oracle/gen_golden.py from the reference.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+PORT_LIB = os.path.join(ROOT, "oracle", "_port", "libbbm_port.so")
+REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libbbm_ref.so")
+
+_libs = {}
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _load(path, prefix):
+    if path not in _libs:
+        if not os.path.exists(path):
+            return None
+        lib = ctypes.CDLL(path)
+        getattr(lib, prefix + "model_name").restype = ctypes.c_char_p
+        _libs[path] = lib
+    return _libs[path]
+
+
+def port():
+    return _load(PORT_LIB, "bbmport_")
+
+
+def ref():
+    return _load(REF_LIB, "bbmref_")
+
+
+def port_models():
+    lib = port()
+    return [lib.bbmport_model_name(i).decode() for i in range(lib.bbmport_num_models())]
+
+
+def _evalpdf(fn, name, params, din, dout, component, unit, nthreads):
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    din = np.ascontiguousarray(din, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n = din.shape[1]
+    res = np.zeros((4, n), np.float32)
+    rc = fn(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(din[0]), _fp(din[1]), _fp(din[2]),
+            _fp(dout[0]), _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component), ctypes.c_uint32(unit), 3,
+            _fp(res[0]), _fp(res[1]), _fp(res[2]), _fp(res[3]), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return res
+
+
+def port_eval_pdf(name, params, din, dout, component=3, unit=0, nthreads=1):
+    """(4, N): eval RGB + pdf from the C restatement."""
+    return _evalpdf(port().bbmport_eval_pdf, name, params, din, dout, component, unit, nthreads)
+
+
+def ref_eval_pdf(name, params, din, dout, component=3, unit=0, nthreads=1):
+    """(4, N): eval RGB + pdf from the reference itself (None if the prebuilt shim is absent)."""
+    lib = ref()
+    if lib is None:
+        return None
+    return _evalpdf(lib.bbmref_eval_pdf, name, params, din, dout, component, unit, nthreads)
+
+
+def _sample(fn, name, params, dout, xi, component, unit, nthreads):
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    xi = np.ascontiguousarray(xi, dtype=np.float32)
+    n = dout.shape[1]
+    res = np.zeros((4, n), np.float32)
+    flag = np.zeros(n, np.uint32)
+    rc = fn(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]),
+            _fp(xi[0]), _fp(xi[1]), ctypes.c_uint32(component), ctypes.c_uint32(unit),
+            _fp(res[0]), _fp(res[1]), _fp(res[2]), _fp(res[3]), _fp(flag), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle cannot sample model {name} (rc={rc})")
+    return res, flag
+
+
+def port_sample(name, params, dout, xi, component=3, unit=0, nthreads=1):
+    return _sample(port().bbmport_sample, name, params, dout, xi, component, unit, nthreads)
+
+
+# ------------------------------------------------------------------------------ golden
+
+def golden_meta():
+    with open(os.path.join(GOLDEN, "models.json")) as f:
+        return json.load(f)
+
+
+def golden_inputs():
+    return np.load(os.path.join(GOLDEN, "inputs.npz"))
+
+
+def golden_model(name):
+    return np.load(os.path.join(GOLDEN, f"{name}.npz"))
+
+
+# ------------------------------------------------------------------------------ comparison
+
+def rel_err(got, ref):
+    """Element-wise relative error; exact agreement (incl. both zero / both NaN) counts as 0."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    same = (got == ref) | (np.isnan(got) & np.isnan(ref))
+    err = np.abs(got - ref) / np.maximum(np.abs(ref), np.finfo(np.float32).tiny)
+    err[same] = 0.0
+    err[np.isnan(err)] = np.inf
+    return err
+
+
+def ulp_diff(got, ref):
+    """|ulp distance| between float32 arrays (NaN == NaN counts as 0)."""
+    a = np.asarray(got, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(ref, np.float32).view(np.int32).astype(np.int64)
+    a = np.where(a < 0, -(a & 0x7FFFFFFF), a)
+    b = np.where(b < 0, -(b & 0x7FFFFFFF), b)
+    d = np.abs(a - b)
+    both_nan = np.isnan(np.asarray(got, np.float32)) & np.isnan(np.asarray(ref, np.float32))
+    d[both_nan] = 0
+    return d
+
+
+# Parity bar (BASELINE.json north_star): |gpu - ref| <= 1e-5 |ref|, with an absolute floor of
+# 1e-6 x max|ref| over the batch for outputs that are ~1e-6 of the batch peak or smaller (values
+# deep in an exponential tail, where one ulp of the exp argument is amplified).
+REL_TOL = 1e-5
+ABS_FLOOR_FRAC = 1e-6
+
+
+def parity_violations(got, ref, rel_tol=REL_TOL, abs_floor_frac=ABS_FLOOR_FRAC):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    finite = np.isfinite(ref)
+    peak = np.max(np.abs(ref[finite])) if finite.any() else 0.0
+    tol = rel_tol * np.abs(ref) + abs_floor_frac * peak
+    ok = (np.abs(got - ref) <= tol) | (got == ref) | (np.isnan(got) & np.isnan(ref))
+    return np.nonzero(~ok)
+
+
+# ------------------------------------------------------------------------------ directions
+
+def dirgen_numpy(seed, stream_id, offset, n, mode=0):
+    """numpy restatement of bbm_hip_fill_directions' counter formula (float64 trig): used to
+    check that shards regenerate disjoint slices of one global batch."""
+    m64 = (1 << 64) - 1
+
+    def mix64(z):
+        z = np.asarray(z, dtype=np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        key = int(mix64(np.uint64(seed & m64))) ^ ((0xd1b54a32d192ed03 * (stream_id + 1)) & m64)
+        idx = np.arange(offset, offset + n, dtype=np.uint64)
+        h = mix64(np.uint64(key) + np.uint64(0x9e3779b97f4a7c15) * idx)
+    u1 = (h >> np.uint64(40)).astype(np.float64) / 16777216.0
+    u2 = ((h >> np.uint64(16)) & np.uint64(0xffffff)).astype(np.float64) / 16777216.0
+    z = u1 if mode == 0 else 2.0 * u1 - 1.0
+    s = np.sqrt(np.maximum(1.0 - z * z, 0.0))
+    phi = 2.0 * np.pi * u2
+    return np.stack([s * np.cos(phi), s * np.sin(phi), z]).astype(np.float32)

@@ -1,0 +1,99 @@
+"""The oracle is pinned before it is trusted (CPU only).
+
+* The C restatement (oracle/port) must reproduce the reference's floatRGB outputs stored in
+  tests/golden (generated from the compiled reference headers) bit for bit.
+* The reference shim itself (oracle/_ref, if prebuilt) must reproduce the fixtures it wrote.
+* Known-answer values printed in the reference's docs (docs/source/use_bsdf.rst:24-43,236-250)
+  and the survey's spot value are checked directly.
+"""
+import numpy as np
+import pytest
+
+from tests import oracle_util as ou
+
+META = ou.golden_meta()
+INP = ou.golden_inputs()
+PORT_MODELS = ou.port_models()
+
+
+def _sets(name):
+    return range(len(META["models"][name]["sets"]))
+
+
+@pytest.mark.parametrize("name", PORT_MODELS)
+def test_port_bit_exact_vs_reference_golden(name):
+    g = ou.golden_model(name)
+    for si in _sets(name):
+        got = ou.port_eval_pdf(name, g[f"params{si}"], INP["pin"], INP["pout"])
+        d = ou.ulp_diff(got, g[f"evalpdf{si}"])
+        assert d.max() == 0, f"{name} set {si}: {np.count_nonzero(d)} values differ (max {d.max()} ulp)"
+
+
+@pytest.mark.parametrize("name", PORT_MODELS)
+@pytest.mark.parametrize("tag,comp,unit", [("diffuse", 1, 0), ("specular", 2, 0), ("importance", 3, 1)])
+def test_port_component_and_unit_masks(name, tag, comp, unit):
+    g = ou.golden_model(name)
+    got = ou.port_eval_pdf(name, g["params0"], INP["pin"], INP["pout"], component=comp, unit=unit)
+    assert ou.ulp_diff(got, g[f"evalpdf_{tag}"]).max() == 0
+
+
+def test_port_lambertian_sample_bit_exact():
+    g = ou.golden_model("Lambertian")
+    for si in _sets("Lambertian"):
+        got, flag = ou.port_sample("Lambertian", g[f"params{si}"], INP["sout"], INP["sxi"])
+        assert ou.ulp_diff(got, g[f"sample{si}"]).max() == 0
+        assert np.array_equal(flag.astype(np.uint8), g[f"sflag{si}"])
+
+
+def test_golden_float_vs_double_spread_is_within_budget():
+    """floatRGB vs doubleRGB of the reference itself: the scale of the 1e-5 parity budget."""
+    for name in ("CookTorrance", "GGX"):
+        g = ou.golden_model(name)
+        f, d = g["evalpdf0"].astype(np.float64), g["evalpdf_double"]
+        sel = np.abs(d) > 1e-6
+        assert (np.abs(f - d)[sel] / np.abs(d[sel])).max() < 1e-5
+
+
+def test_docs_known_answers_lambertian():
+    """docs/source/use_bsdf.rst:24-43 (default Lambertian at in = out = z) and :236-250."""
+    z = np.array([[0.0], [0.0], [1.0]], np.float32)
+    r = ou.port_eval_pdf("Lambertian", [0.5, 0.5, 0.5], z, z)
+    np.testing.assert_allclose(r[:3, 0], [0.159155] * 3, rtol=2e-6)
+    np.testing.assert_allclose(r[3, 0], 0.31831, rtol=2e-5)
+    r = ou.port_eval_pdf("Lambertian", [0.1, 0.2, 0.3], z, z)
+    np.testing.assert_allclose(r[:3, 0], [0.03183099, 0.06366198, 0.09549297], rtol=1e-6)
+    got, flag = ou.port_sample("Lambertian", [0.5, 0.5, 0.5], z, np.array([[0.3], [0.7]], np.float32))
+    np.testing.assert_allclose(got[:3, 0], [-0.169256, 0.520915, 0.83666], atol=2e-6)
+    np.testing.assert_allclose(got[3, 0], 0.266317, rtol=2e-6)
+    assert flag[0] == 1
+
+
+def test_survey_spot_value_cooktorrance():
+    """CookTorrance defaults at in = normalize(0.3,0.1,0.9), out = normalize(-0.2,0.05,0.8)
+    (normalised in float, as bbm::normalize does)."""
+    def nf(v):
+        v = np.asarray(v, np.float32)
+        s = np.float32(0) + v[0] * v[0]
+        s = s + v[1] * v[1]
+        s = s + v[2] * v[2]
+        return (v * (np.float32(1) / np.sqrt(s, dtype=np.float32))).reshape(3, 1)
+    r = ou.port_eval_pdf("CookTorrance", [0.5, 0.5, 0.5, 0.1, 1.3], nf([0.3, 0.1, 0.9]), nf([-0.2, 0.05, 0.8]))
+    assert np.float32(r[0, 0]) == np.float32(0.124202915)
+    assert np.float32(r[3, 0]) == np.float32(10.7763062)
+
+
+@pytest.mark.skipif(ou.ref() is None, reason="oracle/_ref not built")
+def test_reference_shim_reproduces_its_fixtures():
+    for name in META["models"]:
+        g = ou.golden_model(name)
+        got = ou.ref_eval_pdf(name, g["params0"], INP["pin"], INP["pout"])
+        assert ou.ulp_diff(got, g["evalpdf0"]).max() == 0, name
+
+
+def test_dirgen_counter_property():
+    """Slices of one global batch regenerate identically from (seed, offset)."""
+    full = ou.dirgen_numpy(7, 0, 0, 1000, mode=1)
+    part = ou.dirgen_numpy(7, 0, 600, 400, mode=1)
+    assert np.array_equal(full[:, 600:], part)
+    n = np.linalg.norm(full.astype(np.float64), axis=0)
+    np.testing.assert_allclose(n, 1.0, atol=1e-6)
