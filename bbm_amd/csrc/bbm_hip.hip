@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -113,6 +114,17 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
     one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
 }
 
+// Grid cap for the grid-stride kernels; BBM_HIP_MAX_BLOCKS overrides it (tuning experiments).
+uint64_t max_blocks()
+{
+  static const uint64_t v = [] {
+    const char* e = std::getenv("BBM_HIP_MAX_BLOCKS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? uint64_t(x) : uint64_t(kMaxBlocks);
+  }();
+  return v;
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 template<class Model, int MODE, bool MASK>
@@ -125,7 +137,7 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
   const uint64_t units = vec ? (a.n >> 2) : a.n;
   uint64_t blocks = (units + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
-  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks > max_blocks()) blocks = max_blocks();
   if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();
@@ -174,13 +186,13 @@ const ModelEntry kModels[] = {
   {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>,
    {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}},
   {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
   {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,   // bsdfmodel/low.h:32-33
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
   {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
   {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, 1, 5}},
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
 };
 constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
 

@@ -1,0 +1,113 @@
+"""The C-ABI boundary and the host-side mirror of the reference interface (CPU only: no kernel runs).
+
+* libbbm_hip.so loads and exports every symbol declared in include/bbm_hip.h;
+* the registry (names, parameter counts, defaults, bounds) matches the reference's own values
+  recorded in tests/golden/models.json;
+* toString / fromString reproduce bbm::toString byte for byte for every model and parameter set;
+* argument validation fails loudly with the reference's error categories before any launch.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests import oracle_util as ou
+
+ROOT = ou.ROOT
+META = ou.golden_meta()
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "bbm_hip.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(bbm_hip_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from bbm_amd import _lib
+    return _lib.load()
+
+
+def test_header_symbols_exported(lib):
+    syms = _header_symbols()
+    assert len(syms) >= 13
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/bbm_hip.h but not exported"
+
+
+def test_binding_covers_header():
+    from bbm_amd import _lib
+    assert set(_header_symbols()) == set(_lib.SIGNATURES)
+
+
+def test_abi_version(lib):
+    assert lib.bbm_hip_abi_version() == 1
+
+
+def test_registry_matches_reference(lib):
+    from bbm_amd.models import nparams
+    names = [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
+    assert "CookTorrance" in names and "GGX" in names and "Lambertian" in names
+    for i, name in enumerate(names):
+        ref = META["models"][name]
+        assert lib.bbm_hip_model_id(name.encode()) == i
+        k = lib.bbm_hip_model_nparams(i)
+        assert k == ref["nparams"] == nparams(name)
+        buf = (ctypes.c_float * k)()
+        for which, key in ((0, "defaults"), (1, "lower"), (2, "upper")):
+            assert lib.bbm_hip_model_params(i, which, buf, k) == k
+            np.testing.assert_array_equal(np.array(buf[:], np.float32), np.array(ref[key], np.float32), err_msg=f"{name} {key}")
+
+
+def test_python_mirror_layout_covers_every_reference_model():
+    from bbm_amd.models import ATTRIBUTES, nparams
+    for name, ref in META["models"].items():
+        assert name in ATTRIBUTES, name
+        assert nparams(name) == ref["nparams"], name
+
+
+@pytest.mark.parametrize("name", sorted(META["models"]))
+def test_to_string_matches_bbm_toString(name):
+    from bbm_amd.models import to_string
+    g = ou.golden_model(name)
+    for si, s in enumerate(META["models"][name]["strings"]):
+        assert to_string(name, g[f"params{si}"]) == s
+
+
+def test_from_string_round_trip_and_named_args():
+    import bbm_amd
+    for name in bbm_amd.model_names():
+        for s in META["models"][name]["strings"]:
+            m = bbm_amd.fromString(s)
+            assert str(m) == s
+    m = bbm_amd.fromString("CookTorrance(eta = 1.5, roughness = 0.2)")
+    np.testing.assert_array_equal(m.parameter_values(), np.float32([0.5, 0.5, 0.5, 0.2, 1.5]))
+    m = bbm_amd.CookTorrance(albedo=0.25, eta=2.0)
+    assert str(m) == "CookTorrance(albedo = [0.25, 0.25, 0.25], roughness = 0.1, eta = 2)"
+    assert m.attribute("eta") == np.float32(2.0)
+    with pytest.raises(ValueError):
+        bbm_amd.fromString("NoSuchModel(a = 1)")
+    with pytest.raises(TypeError):
+        bbm_amd.CookTorrance(sharpness=3)
+
+
+def test_errors_before_launch(lib):
+    from bbm_amd import _lib
+    p = (ctypes.c_float * 5)(*[0.5, 0.5, 0.5, 0.1, 1.3])
+    # unknown model id -> BBM_HIP_ERR_INVALID_MODEL
+    assert lib.bbm_hip_eval(99, p, 5, *([None] * 7), 0, 3, 0, None, None, None, None) == _lib.ERR_INVALID_MODEL
+    assert b"unknown model" in lib.bbm_hip_last_error()
+    # wrong parameter count -> BBM_HIP_ERR_INVALID_ARG
+    ct = lib.bbm_hip_model_id(b"CookTorrance")
+    assert lib.bbm_hip_eval(ct, p, 4, *([None] * 7), 0, 3, 0, None, None, None, None) == _lib.ERR_INVALID_ARG
+    assert b"expected 5 parameters" in lib.bbm_hip_last_error()
+    # NULL direction pointers with n > 0 -> BBM_HIP_ERR_INVALID_ARG (nothing launched)
+    assert lib.bbm_hip_eval_pdf(ct, p, 5, *([None] * 7), 16, 3, 0, None, None, None, None, None) == _lib.ERR_INVALID_ARG
+    assert lib.bbm_hip_model_id(b"Nope") == _lib.ERR_INVALID_MODEL
+    # n == 0 is a no-op
+    assert lib.bbm_hip_eval_pdf(ct, p, 5, *([None] * 7), 0, 3, 0, None, None, None, None, None) == 0
+    with pytest.raises(_lib.BackboneError):
+        _lib.check(-1)

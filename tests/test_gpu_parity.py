@@ -39,11 +39,34 @@ def _gpu_evalpdf(model, din, dout, **kw):
 
 def _assert_parity(got, ref, what):
     bad = ou.parity_violations(got, ref)
-    assert len(bad[0]) == 0, (f"{what}: {len(bad[0])} values outside tolerance; worst rel "
-                              f"{ou.rel_err(got, ref).max():.3e}")
+    assert len(bad[0]) == 0, (f"{what}: {len(bad[0])} values outside tolerance; e.g. got "
+                              f"{got[bad][:5]} ref {ref[bad][:5]}")
     assert np.array_equal(np.isnan(got), np.isnan(ref)), f"{what}: NaN pattern differs"
-    # masked lanes exactly 0 on both sides
-    assert np.array_equal(got == 0, ref == 0) or ou.rel_err(got, ref).max() < 1e-5
+    # lanes the reference returns exactly 0 for (masked, below horizon, ...) are 0 here too,
+    # except values deep in an underflowing tail (below the absolute floor)
+    finite = np.isfinite(ref)
+    floor = ou.ABS_FLOOR_FRAC * (np.abs(ref[finite]).max() if finite.any() else 0.0)
+    stray = (ref == 0) & (np.abs(got) > floor)
+    assert not stray.any(), f"{what}: {stray.sum()} lanes non-zero where the reference is 0"
+    return _stats(got, ref, floor)
+
+
+def _stats(got, ref, floor):
+    sel = np.abs(ref) > floor
+    rel = ou.rel_err(got, ref)
+    return {"max_ulp": int(ou.ulp_diff(got, ref).max()),
+            "max_rel_above_floor": float(rel[sel].max()) if sel.any() else 0.0,
+            "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0))}
+
+
+def _report(tag, stats):
+    import json
+    import os
+    os.makedirs(os.path.join(ou.ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ou.ROOT, "gpurun_out", f"parity_{tag}.json"), "w") as f:
+        json.dump(stats, f, indent=1)
+    for k, v in stats.items():
+        print(f"{tag} {k}: {v}")
 
 
 def _gpu_models(bbm):
@@ -58,9 +81,8 @@ def test_every_gpu_model_matches_reference_golden(bbm):
             m = bbm.BsdfModel(name)
             m.set_parameter_values(g[f"params{si}"])
             got = _gpu_evalpdf(m, INP["pin"], INP["pout"])
-            _assert_parity(got, g[f"evalpdf{si}"], f"{name}[{si}]")
-            worst[(name, si)] = int(ou.ulp_diff(got, g[f"evalpdf{si}"]).max())
-    print("max ulp vs reference:", worst)
+            worst[f"{name}[{si}]"] = _assert_parity(got, g[f"evalpdf{si}"], f"{name}[{si}]")
+    _report("golden", worst)
 
 
 @pytest.mark.parametrize("tag,comp,unit", [("diffuse", 1, 0), ("specular", 2, 0), ("importance", 3, 1)])
@@ -92,13 +114,15 @@ def test_large_batch_vs_port(bbm):
     din = bbm.fill_directions(0xBB5EED, 0, 0, n, mode=0)
     dout = bbm.fill_directions(0xBB5EED, 1, 0, n, mode=1)
     hin, hout = din.cpu().numpy(), dout.cpu().numpy()
+    stats = {}
     for name in _gpu_models(bbm):
         if name not in ou.port_models():
             continue
         m = bbm.BsdfModel(name)
         got = _gpu_evalpdf(m, hin, hout)
         ref = ou.port_eval_pdf(name, m.parameter_values(), hin, hout, nthreads=8)
-        _assert_parity(got, ref, name)
+        stats[name] = _assert_parity(got, ref, name)
+    _report("large", stats)
 
 
 def test_mask_lanes_are_zero_and_others_untouched(bbm):

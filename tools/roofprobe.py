@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Calibrate the HBM ceiling of the eval+pdf access pattern on the GPU (tools/roofprobe.hip).
+
+    python tools/roofprobe.py [--pairs 100000000]
+
+Prints one line per (variant, grid) with GB/s computed from the algorithmic bytes.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BYTES = {0: 40, 1: 40, 2: 40, 3: 24, 4: 16}
+NAMES = {0: "plain 6in/4out", 1: "nontemporal 6in/4out", 2: "8 pairs/thread 6in/4out", 3: "read-only 6in",
+         4: "write-only 4out"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=100_000_000)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import bbm_amd
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libroofprobe.so"))
+    lib.roofprobe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                              ctypes.c_void_p]
+    n = args.pairs
+    ins = [bbm_amd.fill_directions(1, k, 0, n, mode=1) for k in range(2)]
+    in_rows = [ins[0][0], ins[0][1], ins[0][2], ins[1][0], ins[1][1], ins[1][2]]
+    outs = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(4)]
+    in_ptrs = (ctypes.c_void_p * 6)(*[t.data_ptr() for t in in_rows])
+    out_ptrs = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in outs])
+    s = torch.cuda.current_stream()
+    res = []
+    for v in (0, 1, 2, 3, 4):
+        for blocks in (1024, 2048, 4096, 8192, 16384, (n // 4 + 255) // 256):
+            for _ in range(2):
+                assert lib.roofprobe(v, in_ptrs, out_ptrs, n, blocks, s.cuda_stream) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(args.iters):
+                lib.roofprobe(v, in_ptrs, out_ptrs, n, blocks, s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.iters
+            gbs = BYTES[v] * n / (ms * 1e-3) / 1e9
+            res.append({"variant": v, "name": NAMES[v], "blocks": blocks, "ms": ms, "GBps": gbs})
+            print(f"{NAMES[v]:28s} blocks={blocks:7d} {ms:8.3f} ms {gbs:8.1f} GB/s", flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "roofprobe.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
