@@ -25,7 +25,7 @@ namespace {
 
 constexpr int kMaxParams = 64;
 constexpr int kBlock = 256;
-constexpr int kMaxBlocks = 256 * 8;
+constexpr int kMaxBlocks = 1 << 22;   // effectively one workgroup per 1024 pairs (full grid)
 
 thread_local std::string g_last_error;
 
@@ -61,7 +61,27 @@ __device__ __forceinline__ void one_pair(const Model& m, const EvalArgs& a, uint
 
 // Vector path: 4 consecutive pairs per thread-iteration, 16-byte loads/stores per array.
 // Requires every array 16-byte aligned (checked on the host); the n % 4 tail runs scalar.
-template<class Model, int MODE, bool MASK>
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template<bool NT>
+__device__ __forceinline__ float4 ld4(const float* p, uint64_t t)
+{
+  if (NT)
+  {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p) + t);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return reinterpret_cast<const float4*>(p)[t];
+}
+
+template<bool NT>
+__device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, float c, float d)
+{
+  if (NT) __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
+  else reinterpret_cast<float4*>(p)[t] = make_float4(a, b, c, d);
+}
+
+template<class Model, int MODE, bool MASK, bool NT>
 __global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
 {
   const Model m(a.p.v);
@@ -69,12 +89,12 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
   {
-    const float4 ix = reinterpret_cast<const float4*>(a.ix)[t];
-    const float4 iy = reinterpret_cast<const float4*>(a.iy)[t];
-    const float4 iz = reinterpret_cast<const float4*>(a.iz)[t];
-    const float4 ox = reinterpret_cast<const float4*>(a.ox)[t];
-    const float4 oy = reinterpret_cast<const float4*>(a.oy)[t];
-    const float4 oz = reinterpret_cast<const float4*>(a.oz)[t];
+    const float4 ix = ld4<NT>(a.ix, t);
+    const float4 iy = ld4<NT>(a.iy, t);
+    const float4 iz = ld4<NT>(a.iz, t);
+    const float4 ox = ld4<NT>(a.ox, t);
+    const float4 oy = ld4<NT>(a.oy, t);
+    const float4 oz = ld4<NT>(a.oz, t);
     uint32_t mk = 0x01010101u;
     if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
     const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
@@ -90,11 +110,11 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
     }
     if (MODE & kModeEval)
     {
-      reinterpret_cast<float4*>(a.r)[t] = make_float4(r[0], r[1], r[2], r[3]);
-      reinterpret_cast<float4*>(a.g)[t] = make_float4(g[0], g[1], g[2], g[3]);
-      reinterpret_cast<float4*>(a.b)[t] = make_float4(b[0], b[1], b[2], b[3]);
+      st4<NT>(a.r, t, r[0], r[1], r[2], r[3]);
+      st4<NT>(a.g, t, g[0], g[1], g[2], g[3]);
+      st4<NT>(a.b, t, b[0], b[1], b[2], b[3]);
     }
-    if (MODE & kModePdf) reinterpret_cast<float4*>(a.pdf)[t] = make_float4(p[0], p[1], p[2], p[3]);
+    if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
@@ -125,6 +145,87 @@ uint64_t max_blocks()
   return v;
 }
 
+// Streaming stores/loads with the nontemporal hint (BBM_HIP_NT=0 disables; tuning experiments).
+bool use_nt()
+{
+  static const bool v = [] {
+    const char* e = std::getenv("BBM_HIP_NT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// ------------------------------------------------------------------------------- sample
+
+struct SampleArgs
+{
+  const float* ox; const float* oy; const float* oz;
+  const float* xi0; const float* xi1;
+  const uint8_t* mask;
+  float* dx; float* dy; float* dz; float* pdf; uint32_t* flag;
+  uint64_t n;
+  uint32_t component;
+  ParamBlock p;
+};
+
+template<class Model>
+__device__ __forceinline__ void one_sample(const Model& m, const SampleArgs& a, uint64_t i, bool active)
+{
+  v3 d; float pdf; uint32_t f;
+  m.sample(mk3(a.ox[i], a.oy[i], a.oz[i]), a.xi0[i], a.xi1[i], active ? a.component : 0u, d, pdf, f);
+  a.dx[i] = d.x; a.dy[i] = d.y; a.dz[i] = d.z; a.pdf[i] = pdf; a.flag[i] = f;
+}
+
+// 4 samples per thread-iteration: 5 x 16-byte loads (out xyz, xi0, xi1), 5 x 16-byte stores.
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_sample_v4(SampleArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
+  {
+    const float4 ox = reinterpret_cast<const float4*>(a.ox)[t];
+    const float4 oy = reinterpret_cast<const float4*>(a.oy)[t];
+    const float4 oz = reinterpret_cast<const float4*>(a.oz)[t];
+    const float4 x0 = reinterpret_cast<const float4*>(a.xi0)[t];
+    const float4 x1 = reinterpret_cast<const float4*>(a.xi1)[t];
+    uint32_t mk = 0x01010101u;
+    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
+    const float u0[4] = {x0.x, x0.y, x0.z, x0.w}, u1[4] = {x1.x, x1.y, x1.z, x1.w};
+    float dx[4], dy[4], dz[4], pd[4];
+    uint32_t fl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      v3 d;
+      const uint32_t comp = ((mk >> (8 * j)) & 0xffu) ? a.component : 0u;
+      m.sample(mk3(onx[j], ony[j], onz[j]), u0[j], u1[j], comp, d, pd[j], fl[j]);
+      dx[j] = d.x; dy[j] = d.y; dz[j] = d.z;
+    }
+    reinterpret_cast<float4*>(a.dx)[t] = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    reinterpret_cast<float4*>(a.dy)[t] = make_float4(dy[0], dy[1], dy[2], dy[3]);
+    reinterpret_cast<float4*>(a.dz)[t] = make_float4(dz[0], dz[1], dz[2], dz[3]);
+    reinterpret_cast<float4*>(a.pdf)[t] = make_float4(pd[0], pd[1], pd[2], pd[3]);
+    reinterpret_cast<uint4*>(a.flag)[t] = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_sample<Model>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_sample_v1(SampleArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    one_sample<Model>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 template<class Model, int MODE, bool MASK>
@@ -138,11 +239,35 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
   uint64_t blocks = (units + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
-  if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  if (vec && use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, false>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
   return BBM_HIP_OK;
+}
+
+template<class Model, bool MASK>
+int launch_sample_mask(const SampleArgs& a, hipStream_t s)
+{
+  const bool vec = aligned16(a.ox) && aligned16(a.oy) && aligned16(a.oz) && aligned16(a.xi0) && aligned16(a.xi1) &&
+                   aligned16(a.dx) && aligned16(a.dy) && aligned16(a.dz) && aligned16(a.pdf) && aligned16(a.flag) &&
+                   (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
+  const uint64_t units = vec ? (a.n >> 2) : a.n;
+  uint64_t blocks = (units + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > max_blocks()) blocks = max_blocks();
+  if (vec) hipLaunchKernelGGL((k_sample_v4<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_sample_v1<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+template<class Model>
+int launch_sample(const SampleArgs& a, hipStream_t s)
+{
+  return a.mask ? launch_sample_mask<Model, true>(a, s) : launch_sample_mask<Model, false>(a, s);
 }
 
 template<class Model>
@@ -160,6 +285,7 @@ int launch_eval_pdf(const EvalArgs& a, int mode, hipStream_t s)
 // ------------------------------------------------------------------------ model registry
 
 using EvalLauncher = int (*)(const EvalArgs&, int, hipStream_t);
+using SampleLauncher = int (*)(const SampleArgs&, hipStream_t);
 
 struct ModelEntry
 {
@@ -167,6 +293,7 @@ struct ModelEntry
   int nparams;
   uint32_t components;
   EvalLauncher eval_pdf;
+  SampleLauncher sample;
   float defaults[kMaxParams];
   float lower[kMaxParams];
   float upper[kMaxParams];
@@ -183,15 +310,15 @@ constexpr float kFMax = 3.4028234663852886e+38f;
 // reported by parameter_lower_bound/upper_bound, ior 1.3 in [1,5]); pinned against
 // tests/golden/models.json by tests/test_abi.py.
 const ModelEntry kModels[] = {
-  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>,
+  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>, &launch_sample<Lambertian>,
    {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}},
-  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,
+  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>,   // bsdfmodel/low.h:32-33
+  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>,   // bsdfmodel/low.h:32-33
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>,
+  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>, &launch_sample<GGXM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>,
+  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
 };
 constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
@@ -355,10 +482,23 @@ int bbm_hip_sample(int model_id, const float* params, int nparams,
                    float* dir_x, float* dir_y, float* dir_z, float* pdf, uint32_t* flag,
                    void* stream)
 {
-  (void)params; (void)nparams; (void)out_x; (void)out_y; (void)out_z; (void)xi0; (void)xi1; (void)mask;
-  (void)n; (void)component; (void)unit; (void)dir_x; (void)dir_y; (void)dir_z; (void)pdf; (void)flag; (void)stream;
-  if (!entry(model_id)) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
-  return fail(BBM_HIP_ERR_UNSUPPORTED, "sample is not implemented yet for this model");
+  (void)unit;
+  EvalArgs tmp;
+  const ModelEntry* e;
+  int rc = prepare(model_id, params, nparams, n, tmp, e);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if ((rc = check_dirs(out_x, out_y, out_z, "out"))) return rc;
+  if (!xi0 || !xi1) return fail(BBM_HIP_ERR_INVALID_ARG, "xi pointer is NULL");
+  if (!dir_x || !dir_y || !dir_z || !pdf || !flag) return fail(BBM_HIP_ERR_INVALID_ARG, "sample output pointer is NULL");
+  SampleArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = tmp.p;
+  a.n = n;
+  a.ox = out_x; a.oy = out_y; a.oz = out_z; a.xi0 = xi0; a.xi1 = xi1; a.mask = mask;
+  a.dx = dir_x; a.dy = dir_y; a.dz = dir_z; a.pdf = pdf; a.flag = flag;
+  a.component = component & kFlagAll;
+  return e->sample(a, static_cast<hipStream_t>(stream));
 }
 
 int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,

@@ -23,6 +23,24 @@ struct Lambertian
     rgb[2] = m ? albedo[2] * kInvPiF : 0.0f;
     pdf = m ? in.z * kInvPiF : 0.0f;
   }
+
+  // lambertian.h:76-103 cosine-weighted sampling; sinTheta = safe_sqrt(1.0 - xi1) in double
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f);
+    pdf = 0.0f;
+    flag = kFlagNone;
+    if (!(component & kFlagDiffuse)) return;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+    float s, c;
+    sincosf(xi0 * float(2.0f * kPiD), &s, &c);
+    const float sin_t = float(safe_sqrt(1.0 - xi1));
+    dir = mk3(c * sin_t, s * sin_t, safe_sqrtf(xi1));
+    float rgb[3];
+    eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
+    flag = kFlagDiffuse;
+  }
 };
 
 }  // namespace bbmhip

@@ -33,6 +33,40 @@ struct v2 { float x, y; };
 __device__ __forceinline__ v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
 
+// ---------------------------------------------------------------- division (VALU budget)
+//
+// IEEE division is the dominant VALU cost on this path (hipcc's correctly-rounded f32 divide is
+// ~10 instructions with denormal-mode switches; f64 divide ~11 f64 instructions).  Both are
+// replaced by the hardware reciprocal + Newton/Markstein correction:
+//   q0 = n * rcp(d);  e = fma(-d, q0, n) (exact remainder);  q = fma(e, rcp(d), q0)
+// which returns the correctly rounded quotient except when n/d lies within ~2^-22 ulp of a
+// rounding midpoint (f32; ~2^-100 for the f64 form after two reciprocal refinements), i.e. a
+// 1-ulp difference in roughly one division in four million.  IEEE special cases (d = 0, d = inf,
+// n = inf, NaN) fall back to the uncorrected quotient, which is the IEEE result there.
+// Denormal divisors (|d| < 2^-126) are outside the domain of this path (directions are unit
+// vectors, parameters are >= their documented lower bounds).
+__device__ __forceinline__ float div_nr(float n, float d)
+{
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float q = n * r;
+  const float e = __builtin_fmaf(-d, q, n);
+  const float q1 = __builtin_fmaf(e, r, q);
+  return __builtin_isfinite(q1) ? q1 : q;
+}
+
+__device__ __forceinline__ double ddiv_nr(double n, double d)
+{
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = n * r;
+  const double rem = __builtin_fma(-d, q, n);
+  const double q1 = __builtin_fma(rem, r, q);
+  return __builtin_isfinite(q1) ? q1 : n * __builtin_amdgcn_rcp(d);
+}
+
 // horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2
 __device__ __forceinline__ float dot3(v3 a, v3 b) { return ((0.0f + a.x * b.x) + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float sqnorm2(float a, float b) { return (0.0f + a * a) + b * b; }
@@ -40,7 +74,7 @@ __device__ __forceinline__ float sqnorm2(float a, float b) { return (0.0f + a * 
 // horizontal.h:96-100 normalize = t * rsqrt(|t|^2); math.h:109-112 rsqrt = rcp(sqrt) = 1 / sqrt
 __device__ __forceinline__ v3 normalize3(v3 t)
 {
-  const float r = 1 / sqrtf(dot3(t, t));
+  const float r = div_nr(1.0f, sqrtf(dot3(t, t)));
   return mk3(t.x * r, t.y * r, t.z * r);
 }
 
@@ -60,8 +94,44 @@ __device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 
 // core/spherical.h:79-80 sinTheta2 = bbm::max(1 - z*z, 0) -> fmaxf (result_t<float,int> = float)
 __device__ __forceinline__ float sin_theta2(v3 v) { return fmaxf(1 - v.z * v.z, 0.0f); }
 // spherical.h:179-180 tanTheta = sinTheta / cosTheta; :185-186 tanTheta2 = sinTheta2 / cosTheta2
-__device__ __forceinline__ float tan_theta(v3 v) { return sqrtf(sin_theta2(v)) / v.z; }
-__device__ __forceinline__ float tan_theta2(v3 v) { return sin_theta2(v) / (v.z * v.z); }
+__device__ __forceinline__ float tan_theta(v3 v) { return div_nr(sqrtf(sin_theta2(v)), v.z); }
+__device__ __forceinline__ float tan_theta2(v3 v) { return div_nr(sin_theta2(v), v.z * v.z); }
+
+// std::clamp(a, T(lo), T(hi)) (backbone/native/include/backbone/math.h:106-107)
+__device__ __forceinline__ float clampf(float a, float lo, float hi) { return (a < lo) ? lo : ((hi < a) ? hi : a); }
+
+// core/spherical.h:155-160 cossinPhi: (1, 0) at the pole, else clamp(xy / sinTheta, -1, 1)
+__device__ __forceinline__ void cossin_phi(v3 v, float& c, float& s)
+{
+  const float sT = sqrtf(sin_theta2(v));
+  const float rsT = div_nr(1.0f, sT);
+  if (fabsf(sT) < kEpsF) { c = 1.0f; s = 0.0f; return; }
+  c = clampf(v.x * rsT, -1.0f, 1.0f);
+  s = clampf(v.y * rsT, -1.0f, 1.0f);
+}
+
+// backbone/native/include/backbone/math.h:115-126: Giles' single-precision erfinv polynomial.
+// For T = float the native backbone computes w = -log((1.0 - a)(1.0 + a)) in double and stores it
+// as float, then evaluates the Horner polynomial (util/poly.h:34-38) in double: the result is double.
+__device__ __forceinline__ double erfinv_d(float a)
+{
+  const float w = float(-log((1.0 - a) * (1.0 + a)));
+  if (w < 5)
+  {
+    const double x = w - 2.5;
+    double p = 2.81022636e-08;
+    p = p * x + 3.43273939e-07; p = p * x + -3.5233877e-06; p = p * x + -4.39150654e-06;
+    p = p * x + 0.00021858087; p = p * x + -0.00125372503; p = p * x + -0.00417768164;
+    p = p * x + 0.246640727; p = p * x + 1.50140941;
+    return p * a;
+  }
+  const double x = sqrtf(w) - 3.0;
+  double p = -0.000200214257;
+  p = p * x + 0.000100950558; p = p * x + 0.00134934322; p = p * x + -0.00367342844;
+  p = p * x + 0.00573950773; p = p * x + -0.0076224613; p = p * x + 0.00943887047;
+  p = p * x + 1.00167406; p = p * x + 2.83297682;
+  return p * a;
+}
 
 // bbm::pow(float, int) -> std::pow(float, float); for the exponent 2 used on this path the
 // correctly rounded square is what glibc's powf returns.

@@ -25,8 +25,8 @@ struct Beckmann
   {
     if (!(h.z > 0)) return 0.0f;
     const float c2 = h.z * h.z;
-    const float sn = sqnorm2(h.x / au, h.y / av);
-    float D = expf(-sn / c2) / (au * av * c2 * c2);
+    const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
+    float D = div_nr(expf(div_nr(-sn, c2)), au * av * c2 * c2);
     if (Normalize) D *= kInvPiF;
     return D;
   }
@@ -36,10 +36,39 @@ struct Beckmann
   {
     if (!((v.z > 0) && (dot3(v, m) > 0))) return 0.0f;
     float a;
-    if (Aniso) a = 1 / sqrtf(sqnorm2(v.x * au, v.y * av) / pow2f(v.z));
-    else a = 1 / (au * tan_theta(v));
-    const double g = (a < 1.6) ? (3.535 * a + 2.181 * a * a) / (1 + 2.276 * a + 2.577 * a * a) : 1.0;
-    return float(g);
+    if (Aniso) a = div_nr(1.0f, sqrtf(div_nr(sqnorm2(v.x * au, v.y * av), pow2f(v.z))));
+    else a = div_nr(1.0f, au * tan_theta(v));
+    if (!(a < 1.6)) return 1.0f;
+    const double ad = a;
+    return float(ddiv_nr(3.535 * ad + 2.181 * ad * ad, 1 + 2.276 * ad + 2.577 * ad * ad));
+  }
+
+  // beckmann.h:76-116: visible-normal sampling following [Jakob 2014] (stretch, invert the
+  // slope CDF with three Newton steps on erfinv, rotate, unstretch)
+  __device__ __forceinline__ v3 sample(v3 view, float xi0, float xi1) const
+  {
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
+    const v3 vs = normalize3(mk3(view.x * au, view.y * av, view.z));
+    const float tanT = tan_theta(vs);
+    const float maxval = erff(div_nr(1.0f, tanT));
+    float xc0 = clampf(xi0, float(10e-6), float(1.0 - 10e-6));
+    const float xc1 = clampf(xi1, float(10e-6), float(1.0 - 10e-6));
+    float x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
+    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf(-(vs.z * vs.z))));
+    for (int i = 0; i < 3; ++i)
+    {
+      const float slope = float(erfinv_d(x));
+      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf(-slope * slope) - xc0);
+      const float der = float(1.0 - slope * tanT);
+      x -= div_nr(val, der);
+    }
+    float s0 = 0.0f, s1 = 0.0f;
+    if (x > -1.0 && x < +1.0) { s0 = float(erfinv_d(x)); s1 = float(erfinv_d(float(2.0 * xc1 - 1.0))); }
+    float c, s;
+    cossin_phi(vs, c, s);
+    const float u0 = ((0.0f + c * s0) + -s * s1) * au;
+    const float u1 = ((0.0f + s * s0) + c * s1) * av;
+    return normalize3(mk3(-u0, -u1, 1.0f));
   }
 };
 
@@ -56,10 +85,10 @@ struct GGX
   {
     if (!(h.z > 0)) return 0.0f;
     const float alpha2 = (1.0f * au) * av;
-    const float s = sqnorm2(h.x / au, h.y / av) + pow2f(h.z);
+    const float s = sqnorm2(div_nr(h.x, au), div_nr(h.y, av)) + pow2f(h.z);
     const double sd = double(s);
-    const double d = kPiF * alpha2 * (sd * sd);
-    return float(1 / d);
+    const double d = double(kPiF * alpha2) * (sd * sd);
+    return float(ddiv_nr(1.0, d));
   }
 
   // ggx.h:173-189: 2 / (1 + sqrt(1 + alpha^2 tan^2)) with `Value denom` rounding to float
@@ -68,7 +97,29 @@ struct GGX
     if (!((v.z > 0) && (dot3(v, m) > 0))) return 0.0f;
     const float r2 = (1.0f * au) * av;
     const float denom = float(1.0 + sqrt(1.0 + r2 * tan_theta2(v)));
-    return float(2.0 / denom);
+    // 2.0 / denom rounded to float: one IEEE op on float operands evaluated in double and rounded
+    // once more to float is the float op itself (53 >= 2*24+2: double rounding is innocuous)
+    return div_nr(2.0f, denom);
+  }
+
+  // ggx.h:84-108: visible-normal sampling following [Heitz 2017]
+  __device__ __forceinline__ v3 sample(v3 view, float xi0, float xi1) const
+  {
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
+    const v3 vs = normalize3(mk3(view.x * au, view.y * av, view.z));
+    const v3 T1 = (vs.z < 1.0 - kEpsF) ? normalize3(cross3(vs, mk3(0.0f, 0.0f, 1.0f))) : mk3(1.0f, 0.0f, 0.0f);
+    const v3 T2 = cross3(T1, vs);
+    const float a = float(ddiv_nr(1.0, 1.0 + vs.z));
+    const float r = sqrtf(xi0);
+    const float phi = float(((xi1 < a) ? double(div_nr(xi1, a)) : 1.0 + ddiv_nr(double(xi1 - a), 1.0 - a)) * kPiF);
+    float sp, cp;
+    sincosf(phi, &sp, &cp);
+    const float P1 = r * cp;
+    const float P2 = float(((xi1 < a) ? 1.0 : double(vs.z)) * r * sp);
+    const float sq = float(safe_sqrt(1.0 - P1 * P1 - P2 * P2));
+    const v3 n = mk3((T1.x * P1 + T2.x * P2) + vs.x * sq, (T1.y * P1 + T2.y * P2) + vs.y * sq,
+                     (T1.z * P1 + T2.z * P2) + vs.z * sq);
+    return normalize3(mk3(n.x * au, n.y * av, float(fmax(0.0, double(n.z)))));
   }
 };
 
@@ -80,7 +131,7 @@ __device__ __forceinline__ float vndf_pdf(const NDF& ndf, v3 view, v3 m, float D
 {
   if (!(m.z > 0)) return 0.0f;
   float pdf = D;
-  pdf *= ndf.G1(view, m) * fabsf(dot3(view, m)) / view.z;
+  pdf *= div_nr(ndf.G1(view, m) * fabsf(dot3(view, m)), view.z);
   if (!(pdf > 0)) return 0.0f;
   return pdf;
 }
@@ -95,9 +146,14 @@ struct VGroove
   __device__ __forceinline__ static float eval(const NDF&, v3 in, v3 out, v3 m, float inm, float outm)
   {
     if (!((inm > 0) && (outm > 0))) return 0.0f;
-    const double gi = 2.0 * m.z * in.z / inm;
-    const double go = 2.0 * m.z * out.z / outm;
-    return float(fmin(1.0, fmin(gi, go)));
+    // min(1, Pi/inm, Po/outm) with Pi = 2 z_m z_in exact in double: the comparisons with 1 are
+    // exact (Pi < inm), so only the smaller ratio is ever divided -- one division, not two.
+    const double pi = 2.0 * m.z * in.z, po = 2.0 * m.z * out.z;
+    const double di = inm, dd = outm;
+    const bool li = pi < di, lo = po < dd;
+    if (!li && !lo) return 1.0f;
+    const bool use_i = li && (!lo || pi * dd <= po * di);
+    return float(ddiv_nr(use_i ? pi : po, use_i ? di : dd));
   }
 };
 
@@ -123,9 +179,9 @@ struct FresnelCook
   __device__ __forceinline__ float eval(float c) const
   {
     const float g = safe_sqrtf(eta * eta + c * c - 1.0f);
-    const float a = (g - c) / (g + c);
-    const float b = (c * (g + c) - 1.0f) / (c * (g - c) + 1.0f);
-    return float(fmax(double(0.5f * (a * a) * (1.0f + b * b)), 0.0));   // bbm::max(x, 0.0)
+    const float a = div_nr(g - c, g + c);
+    const float b = div_nr(c * (g + c) - 1.0f, c * (g - c) + 1.0f);
+    return fmaxf(0.5f * (a * a) * (1.0f + b * b), 0.0f);   // bbm::max(x, 0.0): fmax in double == fmaxf here
   }
 };
 
@@ -139,6 +195,17 @@ template<> struct norm_value<Norm::Walter> { static constexpr double v = 4.0; };
 template<> struct norm_value<Norm::Cook> { static constexpr double v = kPiD; };
 
 enum : int { kModeEval = 1, kModePdf = 2, kModeEvalPdf = 3 };
+
+// float((x / NormalizationFactor) / y) for float x, y (microfacet.h:100).  Walter (4.0) and
+// Unnormalized divide exactly by a power of two, so the double expression is one float division;
+// Cook (pi) keeps a double quotient x / (pi * y) -- within 2 double ulp of the reference's
+// two-step quotient, so the float result differs only if it sits within 2^-28 of a float midpoint.
+template<Norm N>
+__device__ __forceinline__ float eval_scale(float x, float y)
+{
+  if (N == Norm::Cook) return float(ddiv_nr(double(x), kPiD * double(y)));
+  return div_nr(N == Norm::Walter ? x * 0.25f : x, y);
+}
 
 template<class NDF, class MS, class FRESNEL, Norm N, bool Scaled>
 struct Microfacet
@@ -174,7 +241,7 @@ struct Microfacet
       const float G = MS::eval(ndf, in, out, h, inh, outh);
       const float F = fresnel.eval(0.5f * (inh + outh));
       // (D G F) / NormalizationFactor / (z_in z_out): literal<double> promotes to double
-      const float res = float(D * G * F / norm_value<N>::v / (in.z * out.z));
+      const float res = eval_scale<N>(D * G * F, in.z * out.z);
       if (Scaled) { rgb[0] = res * albedo[0]; rgb[1] = res * albedo[1]; rgb[2] = res * albedo[2]; }
       else { rgb[0] = rgb[1] = rgb[2] = res; }
     }
@@ -183,10 +250,31 @@ struct Microfacet
       if (h.z < 0)   // microfacet.h:167 -- unreachable for z_in, z_out > 0 but kept for NaN-free parity
       {
         const v3 hf = neg3(h);
-        pdf = float(vndf_pdf(ndf, out, hf, ndf.eval(hf)) / (4.0 * fabsf(dot3(out, hf))));
+        pdf = div_nr(vndf_pdf(ndf, out, hf, ndf.eval(hf)), 4.0f * fabsf(dot3(out, hf)));
       }
-      else pdf = float(vndf_pdf(ndf, out, h, D) / (4.0 * fabsf(outh)));
+      // float(p / (4.0 * |o.h|)): float operands, one double op -> identical to the float division
+      else pdf = div_nr(vndf_pdf(ndf, out, h, D), 4.0f * fabsf(outh));
     }
+  }
+
+  // microfacet.h:115-141 sample: m ~ VNDF(out), direction = reflect(out, m)
+  // (core/vec_transform.h:43-44, `m * dot(m, out) * 2.0 - out`: the double subtraction of two float
+  // values rounded to float is the float subtraction), pdf = microfacet pdf of that direction.
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f);
+    pdf = 0.0f;
+    flag = kFlagNone;
+    if (!(component & kFlagSpecular)) return;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+    if (!(out.z > 0)) return;
+    const v3 m = ndf.sample(out, xi0, xi1);
+    const float d = dot3(m, out);
+    dir = mk3(2.0f * (m.x * d) - out.x, 2.0f * (m.y * d) - out.y, 2.0f * (m.z * d) - out.z);
+    float rgb[3];
+    eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
   }
 };
 

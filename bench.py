@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BYTES_PER_PAIR = 40           # 24 B in + 16 B out (eval RGB + pdf), f32 SoA
+# models whose eval+pdf never reads in.xy / out.xy: only z is loaded (8 B in + 16 B out)
+BYTES_PER_PAIR_MODEL = {"Lambertian": 24}
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec
 SEED = 0xBB5EED
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
@@ -138,7 +140,8 @@ def main():
 
     if rank == 0:
         total_pairs = n * world * args.steps
-        achieved = BYTES_PER_PAIR * n / (kern_ms * 1e-3) / 1e9
+        bpp = BYTES_PER_PAIR_MODEL.get(args.model, BYTES_PER_PAIR)
+        achieved = bpp * n / (kern_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
             try:
@@ -168,7 +171,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"k_eval_pdf_v4<{args.model}>", "kernel_ms": kern_ms,
-                         "bytes_per_pair": BYTES_PER_PAIR},
+                         "bytes_per_pair": bpp},
             "outputs_ok": ok,
         }
         if world == 1 and not args.no_cpu:

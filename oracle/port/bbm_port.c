@@ -233,6 +233,126 @@ static void lambertian_sample(v3 out, float xi0, float xi1, uint32_t comp, v3* d
   *flag = FLAG_DIFFUSE;
 }
 
+
+/* ---------------------------------------------------------------- sampling */
+
+static const float kInvSqrtPiF = (float)(1.0f * 0.564189583547756286948079451560772586);
+static const float kEpsF = 1.1920928955078125e-07f;
+
+/* std::clamp(a, T(lo), T(hi)) (backbone/native/include/backbone/math.h:106-107) */
+static inline float clampf(float a, float lo, float hi) { return (a < lo) ? lo : ((hi < a) ? hi : a); }
+
+/* backbone/native/include/backbone/math.h:115-126: Giles' erfinv; w rounds to T, the Horner
+   polynomial (util/poly.h:34-38) runs in double and the result stays double */
+static double erfinv_d(float a)
+{
+  float w = (float)(-log((1.0 - a) * (1.0 + a)));
+  if (w < 5)
+  {
+    double x = w - 2.5;
+    double p = 2.81022636e-08;
+    p = p * x + 3.43273939e-07; p = p * x + -3.5233877e-06; p = p * x + -4.39150654e-06;
+    p = p * x + 0.00021858087; p = p * x + -0.00125372503; p = p * x + -0.00417768164;
+    p = p * x + 0.246640727; p = p * x + 1.50140941;
+    return p * a;
+  }
+  double x = sqrtf(w) - 3.0;
+  double p = -0.000200214257;
+  p = p * x + 0.000100950558; p = p * x + 0.00134934322; p = p * x + -0.00367342844;
+  p = p * x + 0.00573950773; p = p * x + -0.0076224613; p = p * x + 0.00943887047;
+  p = p * x + 1.00167406; p = p * x + 2.83297682;
+  return p * a;
+}
+
+/* core/spherical.h:155-160 cossinPhi */
+static inline void cossin_phi(v3 v, float* c, float* s)
+{
+  float sT = sqrtf(sin_theta2(v));
+  float rsT = 1 / sT;
+  if (fabsf(sT) < kEpsF) { *c = 1; *s = 0; return; }
+  *c = clampf(v.x * rsT, -1.0f, 1.0f);
+  *s = clampf(v.y * rsT, -1.0f, 1.0f);
+}
+
+static inline v3 cross3(v3 a, v3 b)
+{
+  v3 r = { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x };
+  return r;
+}
+
+/* ndf/beckmann.h:76-116 VNDF sampling following [Jakob 2014] */
+static v3 beckmann_sample(v3 view, float xi0, float xi1, float au, float av)
+{
+  v3 zero = { 0, 0, 0 };
+  if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return zero;
+  v3 st = { view.x * au, view.y * av, view.z };
+  v3 vs = normalize3(st);
+  float tanT = tan_theta(vs);
+  float maxval = erff(1 / tanT);
+  float xc0 = clampf(xi0, (float)10e-6, (float)(1.0 - 10e-6));
+  float xc1 = clampf(xi1, (float)10e-6, (float)(1.0 - 10e-6));
+  float x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
+  xc0 = (float)(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf(-(vs.z * vs.z))));
+  for (int i = 0; i < 3; ++i)
+  {
+    float slope = (float)erfinv_d(x);
+    float val = (float)(1.0 + x + kInvSqrtPiF * tanT * expf(-slope * slope) - xc0);
+    float der = (float)(1.0 - slope * tanT);
+    x -= val / der;
+  }
+  float s0 = 0, s1 = 0;
+  float t1 = (float)(2.0 * xc1 - 1.0);
+  double e0 = erfinv_d(x), e1 = erfinv_d(t1);
+  if (x > -1.0 && x < +1.0) { s0 = (float)e0; s1 = (float)e1; }
+  float c, s;
+  cossin_phi(vs, &c, &s);
+  float u0 = ((0.0f + c * s0) + -s * s1) * au;
+  float u1 = ((0.0f + s * s0) + c * s1) * av;
+  v3 m = { -u0, -u1, 1 };
+  return normalize3(m);
+}
+
+/* ndf/ggx.h:84-108 VNDF sampling following [Heitz 2017] */
+static v3 ggx_sample(v3 view, float xi0, float xi1, float au, float av)
+{
+  v3 zero = { 0, 0, 0 };
+  if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return zero;
+  v3 st = { view.x * au, view.y * av, view.z };
+  v3 vs = normalize3(st);
+  v3 ez = { 0, 0, 1 }, ex = { 1, 0, 0 };
+  v3 T1 = (vs.z < 1.0 - kEpsF) ? normalize3(cross3(vs, ez)) : ex;
+  v3 T2 = cross3(T1, vs);
+  float a = (float)(1 / (1.0 + vs.z));
+  float r = sqrtf(xi0);
+  float phi = (float)(((xi1 < a) ? (double)(xi1 / a) : 1.0 + (xi1 - a) / (1.0 - a)) * kPiF);
+  float cp = cosf(phi), sp = sinf(phi);
+  float P1 = r * cp;
+  float P2 = (float)(((xi1 < a) ? 1.0 : (double)vs.z) * r * sp);
+  float sq = (float)safe_sqrt(1.0 - P1 * P1 - P2 * P2);
+  v3 nrm = { (T1.x * P1 + T2.x * P2) + vs.x * sq, (T1.y * P1 + T2.y * P2) + vs.y * sq,
+             (T1.z * P1 + T2.z * P2) + vs.z * sq };
+  v3 un = { nrm.x * au, nrm.y * av, (float)fmax(0.0, (double)nrm.z) };
+  return normalize3(un);
+}
+
+/* bsdfmodel/microfacet.h:115-141 sample: reflect(out, m) (core/vec_transform.h:43-44), pdf */
+static void microfacet_sample(const microfacet_desc* d, const float* p, v3 out, float xi0, float xi1, uint32_t comp,
+                              v3* dir, float* pdf, uint32_t* flag)
+{
+  dir->x = dir->y = dir->z = 0; *pdf = 0; *flag = FLAG_NONE;
+  if (!(comp & FLAG_SPECULAR)) return;
+  if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+  if (!(out.z > 0)) return;
+  const float au = p[3], av = d->aniso ? p[4] : p[3];
+  v3 m = (d->ndf == NDF_GGX) ? ggx_sample(out, xi0, xi1, au, av) : beckmann_sample(out, xi0, xi1, au, av);
+  float dm = dot3(m, out);
+  dir->x = (float)((double)(m.x * dm) * 2.0 - out.x);
+  dir->y = (float)((double)(m.y * dm) * 2.0 - out.y);
+  dir->z = (float)((double)(m.z * dm) * 2.0 - out.z);
+  *pdf = microfacet_pdf(d, p, *dir, out, comp);
+  *flag = FLAG_SPECULAR;
+}
+
 /* ---------------------------------------------------------------- dispatch */
 
 enum { M_LAMBERTIAN = -1 };
@@ -285,14 +405,16 @@ int bbmport_sample(const char* name, const float* params, int nparams, size_t n,
                    const float* xi0, const float* xi1, uint32_t component, uint32_t unit,
                    float* dx, float* dy, float* dz, float* pdf, uint32_t* flag, int nthreads)
 {
-  (void)unit; (void)nparams; (void)params;
+  (void)unit; (void)nparams;
   int m = find_model(name);
-  if (m != M_LAMBERTIAN) return -2;   /* microfacet sampling: see DESIGN.md (next row) */
+  if (m == -1000) return -1;
+  const microfacet_desc* d = (m >= 0) ? &kMicrofacet[m] : 0;
   #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
   for (long long i = 0; i < (long long)n; ++i)
   {
     v3 out = { ox[i], oy[i], oz[i] }, dir;
-    lambertian_sample(out, xi0[i], xi1[i], component, &dir, &pdf[i], &flag[i]);
+    if (d) microfacet_sample(d, params, out, xi0[i], xi1[i], component, &dir, &pdf[i], &flag[i]);
+    else lambertian_sample(out, xi0[i], xi1[i], component, &dir, &pdf[i], &flag[i]);
     dx[i] = dir.x; dy[i] = dir.y; dz[i] = dir.z;
   }
   return 0;

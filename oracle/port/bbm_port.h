@@ -4,7 +4,7 @@
  * eval/pdf/sample path.  Used only by tests/ (as a checker) and by bench.py's cpu_baseline leg
  * when the prebuilt reference harness is absent.  Never linked into the product (bbm_amd/).
  *
- * Pinned against the reference's own outputs: tests/golden/*.npz (generated from the compiled
+ * Pinned against the reference's own outputs: tests/golden/ (npz) (generated from the compiled
  * reference headers by oracle/gen_golden.py) -- see tests/test_oracle.py.
  *
  * Entry points mirror oracle/ref_harness.cpp so the two libraries are interchangeable.
