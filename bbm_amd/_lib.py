@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbbm_hip.so")
+LIB_PATH = os.environ.get("BBM_HIP_LIB") or os.path.join(_HERE, "lib", "libbbm_hip.so")
 
 # return codes (include/bbm_hip.h)
 OK = 0

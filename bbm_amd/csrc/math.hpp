@@ -67,6 +67,44 @@ __device__ __forceinline__ double ddiv_nr(double n, double d)
   return __builtin_isfinite(q1) ? q1 : n * __builtin_amdgcn_rcp(d);
 }
 
+// float(n / d) for double n, d -- the reference's double-promoted quotients that are immediately
+// stored into a float (e.g. maskingshadowing/vgroove.h:41-44, ndf/beckmann.h:196).  An f32
+// reciprocal estimate (rel. error ~2^-22) plus one f64 remainder correction gives the quotient to
+// ~2^-45, so the float rounding agrees with the reference except within ~2^-21 ulp of a midpoint;
+// two f64 FMAs instead of a full f64 division.
+__device__ __forceinline__ float f_div_d(double n, double d)
+{
+  const float r = __builtin_amdgcn_rcpf(float(d));
+  const double q0 = double(float(n) * r);
+  const double rem = __builtin_fma(-d, q0, n);
+  const double q = __builtin_fma(rem, double(r), q0);
+  return __builtin_isfinite(q) ? float(q) : float(n) * r;   // d = 0 / inf, n = inf: IEEE result
+}
+
+// ---------------------------------------------------------------- compensated f32 (double-float)
+//
+// Where the reference promotes to double only to form a product of two floats and divide it
+// (e.g. vgroove's `2.0 * z_m * z_in / dot`), the exact product is carried as an unevaluated f32
+// pair (hi + lo, Dekker/FMA two-product) and the quotient is corrected with the low part: the
+// result is the float nearest the exact quotient (to ~2^-45), which is what rounding the
+// reference's double quotient to float gives -- all in full-rate f32 instead of half-rate f64.
+__device__ __forceinline__ void two_prod(float a, float b, float& hi, float& lo)
+{
+  hi = a * b;
+  lo = __builtin_fmaf(a, b, -hi);
+}
+
+// float nearest (nh + nl) / (dh + dl), |nl| <= ulp(nh)/2, |dl| <= ulp(dh)/2
+__device__ __forceinline__ float div_ff(float nh, float nl, float dh, float dl)
+{
+  const float r = __builtin_amdgcn_rcpf(dh);
+  float q = nh * r;
+  q = __builtin_fmaf(__builtin_fmaf(-dh, q, nh), r, q);           // ~correctly rounded nh / dh
+  const float rem = __builtin_fmaf(-dh, q, nh) + __builtin_fmaf(-q, dl, nl);
+  const float q1 = __builtin_fmaf(rem, r, q);
+  return __builtin_isfinite(q1) ? q1 : nh * r;
+}
+
 // horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2
 __device__ __forceinline__ float dot3(v3 a, v3 b) { return ((0.0f + a.x * b.x) + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float sqnorm2(float a, float b) { return (0.0f + a * a) + b * b; }

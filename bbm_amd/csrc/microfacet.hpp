@@ -23,24 +23,23 @@ struct Beckmann
   // beckmann.h:49-66: exp(-|h.xy/alpha|^2 / cos^2) / (au av cos^4) [x 1/pi if Normalize]
   __device__ __forceinline__ float eval(v3 h) const
   {
-    if (!(h.z > 0)) return 0.0f;
     const float c2 = h.z * h.z;
     const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
     float D = div_nr(expf(div_nr(-sn, c2)), au * av * c2 * c2);
     if (Normalize) D *= kInvPiF;
-    return D;
+    return (h.z > 0) ? D : 0.0f;
   }
 
   // beckmann.h:180-201: Walter's rational approximation of the Smith G1 term
   __device__ __forceinline__ float G1(v3 v, v3 m) const
   {
-    if (!((v.z > 0) && (dot3(v, m) > 0))) return 0.0f;
+    const bool mask = (v.z > 0) && (dot3(v, m) > 0);
     float a;
     if (Aniso) a = div_nr(1.0f, sqrtf(div_nr(sqnorm2(v.x * au, v.y * av), pow2f(v.z))));
     else a = div_nr(1.0f, au * tan_theta(v));
-    if (!(a < 1.6)) return 1.0f;
     const double ad = a;
-    return float(ddiv_nr(3.535 * ad + 2.181 * ad * ad, 1 + 2.276 * ad + 2.577 * ad * ad));
+    const float g = f_div_d(3.535 * ad + 2.181 * ad * ad, 1 + 2.276 * ad + 2.577 * ad * ad);
+    return mask ? ((a < 1.6) ? g : 1.0f) : 0.0f;
   }
 
   // beckmann.h:76-116: visible-normal sampling following [Jakob 2014] (stretch, invert the
@@ -83,23 +82,22 @@ struct GGX
   // ggx.h:50-65: rcp(Pi * alpha2 * pow(|h.xy/alpha|^2 + pow(z,2), 2.0)) -- the outer pow in double
   __device__ __forceinline__ float eval(v3 h) const
   {
-    if (!(h.z > 0)) return 0.0f;
     const float alpha2 = (1.0f * au) * av;
     const float s = sqnorm2(div_nr(h.x, au), div_nr(h.y, av)) + pow2f(h.z);
     const double sd = double(s);
     const double d = double(kPiF * alpha2) * (sd * sd);
-    return float(ddiv_nr(1.0, d));
+    return (h.z > 0) ? f_div_d(1.0, d) : 0.0f;
   }
 
   // ggx.h:173-189: 2 / (1 + sqrt(1 + alpha^2 tan^2)) with `Value denom` rounding to float
   __device__ __forceinline__ float G1(v3 v, v3 m) const
   {
-    if (!((v.z > 0) && (dot3(v, m) > 0))) return 0.0f;
+    const bool mask = (v.z > 0) && (dot3(v, m) > 0);
     const float r2 = (1.0f * au) * av;
     const float denom = float(1.0 + sqrt(1.0 + r2 * tan_theta2(v)));
     // 2.0 / denom rounded to float: one IEEE op on float operands evaluated in double and rounded
     // once more to float is the float op itself (53 >= 2*24+2: double rounding is innocuous)
-    return div_nr(2.0f, denom);
+    return mask ? div_nr(2.0f, denom) : 0.0f;
   }
 
   // ggx.h:84-108: visible-normal sampling following [Heitz 2017]
@@ -129,11 +127,9 @@ struct GGX
 template<class NDF>
 __device__ __forceinline__ float vndf_pdf(const NDF& ndf, v3 view, v3 m, float D)
 {
-  if (!(m.z > 0)) return 0.0f;
   float pdf = D;
   pdf *= div_nr(ndf.G1(view, m) * fabsf(dot3(view, m)), view.z);
-  if (!(pdf > 0)) return 0.0f;
-  return pdf;
+  return ((m.z > 0) && (pdf > 0)) ? pdf : 0.0f;
 }
 
 // ---------------------------------------------------------------------- masking-shadowing
@@ -145,15 +141,18 @@ struct VGroove
   template<class NDF>
   __device__ __forceinline__ static float eval(const NDF&, v3 in, v3 out, v3 m, float inm, float outm)
   {
-    if (!((inm > 0) && (outm > 0))) return 0.0f;
-    // min(1, Pi/inm, Po/outm) with Pi = 2 z_m z_in exact in double: the comparisons with 1 are
-    // exact (Pi < inm), so only the smaller ratio is ever divided -- one division, not two.
-    const double pi = 2.0 * m.z * in.z, po = 2.0 * m.z * out.z;
-    const double di = inm, dd = outm;
-    const bool li = pi < di, lo = po < dd;
-    if (!li && !lo) return 1.0f;
-    const bool use_i = li && (!lo || pi * dd <= po * di);
-    return float(ddiv_nr(use_i ? pi : po, use_i ? di : dd));
+    // min(1, Pi/inm, Po/outm) with Pi = 2 z_m z_in, exact in double in the reference; here the exact
+    // product is an f32 pair (2 z_m is exact), the comparisons with 1 are exact, and only the
+    // smaller ratio is divided -- one compensated f32 division, no f64.
+    const float tm = 2.0f * m.z;
+    float pih, pil, poh, pol;
+    two_prod(tm, in.z, pih, pil);
+    two_prod(tm, out.z, poh, pol);
+    const bool li = (pih < inm) || (pih == inm && pil < 0.0f);
+    const bool lo = (poh < outm) || (poh == outm && pol < 0.0f);
+    const bool use_i = li && (!lo || pih * outm <= poh * inm);
+    const float g = div_ff(use_i ? pih : poh, use_i ? pil : pol, use_i ? inm : outm, 0.0f);
+    return ((inm > 0) && (outm > 0)) ? ((li || lo) ? g : 1.0f) : 0.0f;
   }
 };
 
@@ -163,8 +162,8 @@ struct Uncorrelated
   template<class NDF>
   __device__ __forceinline__ static float eval(const NDF& ndf, v3 in, v3 out, v3 m, float inm, float outm)
   {
-    if (!((inm > 0) && (outm > 0))) return 0.0f;
-    return ndf.G1(in, m) * ndf.G1(out, m);
+    const float g = ndf.G1(in, m) * ndf.G1(out, m);
+    return ((inm > 0) && (outm > 0)) ? g : 0.0f;
   }
 };
 
@@ -197,13 +196,23 @@ template<> struct norm_value<Norm::Cook> { static constexpr double v = kPiD; };
 enum : int { kModeEval = 1, kModePdf = 2, kModeEvalPdf = 3 };
 
 // float((x / NormalizationFactor) / y) for float x, y (microfacet.h:100).  Walter (4.0) and
-// Unnormalized divide exactly by a power of two, so the double expression is one float division;
-// Cook (pi) keeps a double quotient x / (pi * y) -- within 2 double ulp of the reference's
-// two-step quotient, so the float result differs only if it sits within 2^-28 of a float midpoint.
+// Unnormalized divide exactly by a power of two, so the double expression is one float division.
+// Cook (pi): the reference's two double quotients are within ~2^-52 of x / (pi y); here pi y is
+// formed as an f32 pair (pi = kPiHi + kPiLo to ~2^-48) and divided with the compensated f32
+// quotient, so the float result agrees except within ~2^-20 ulp of a rounding midpoint.
+constexpr float kPiHi = 3.14159274101257324f;    // RN_f(pi)
+constexpr float kPiLo = -8.74227766e-08f;        // RN_f(pi - kPiHi)
+
 template<Norm N>
 __device__ __forceinline__ float eval_scale(float x, float y)
 {
-  if (N == Norm::Cook) return float(ddiv_nr(double(x), kPiD * double(y)));
+  if (N == Norm::Cook)
+  {
+    float dh, dl;
+    two_prod(y, kPiHi, dh, dl);
+    dl = __builtin_fmaf(y, kPiLo, dl);
+    return div_ff(x, 0.0f, dh, dl);
+  }
   return div_nr(N == Norm::Walter ? x * 0.25f : x, y);
 }
 
@@ -228,11 +237,14 @@ struct Microfacet
   template<int MODE>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
-    rgb[0] = rgb[1] = rgb[2] = 0.0f;
-    pdf = 0.0f;
-    if (!(component & kFlagSpecular)) return;
-    if (!((in.z > 0.0f) && (out.z > 0.0f))) return;   // eval :80 and pdf :163 use the same test
+    // Branch-free: every term is computed and the masks are applied with selects, so the four
+    // pairs a thread owns share one basic block and the scheduler interleaves them (this hides
+    // the VALU->mask and transcendental hazards that otherwise cost an s_nop per compare).
+    // eval :77-83 and pdf :160-164 test the same lanes: Specular component, z_in > 0, z_out > 0.
+    const bool active = (component & kFlagSpecular) && (in.z > 0.0f) && (out.z > 0.0f);
     const v3 h = halfway(in, out);
+    // pdf's `h = z(h) < 0 ? -h : h` (:167) never fires on active lanes: z(in + out) > 0 and
+    // normalize scales by a positive factor, so h is used as is.
     const float D = ndf.eval(h);
     const float outh = dot3(out, h);
     if (MODE & kModeEval)
@@ -242,19 +254,18 @@ struct Microfacet
       const float F = fresnel.eval(0.5f * (inh + outh));
       // (D G F) / NormalizationFactor / (z_in z_out): literal<double> promotes to double
       const float res = eval_scale<N>(D * G * F, in.z * out.z);
-      if (Scaled) { rgb[0] = res * albedo[0]; rgb[1] = res * albedo[1]; rgb[2] = res * albedo[2]; }
-      else { rgb[0] = rgb[1] = rgb[2] = res; }
+      rgb[0] = active ? (Scaled ? res * albedo[0] : res) : 0.0f;
+      rgb[1] = active ? (Scaled ? res * albedo[1] : res) : 0.0f;
+      rgb[2] = active ? (Scaled ? res * albedo[2] : res) : 0.0f;
     }
+    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
     if (MODE & kModePdf)
     {
-      if (h.z < 0)   // microfacet.h:167 -- unreachable for z_in, z_out > 0 but kept for NaN-free parity
-      {
-        const v3 hf = neg3(h);
-        pdf = div_nr(vndf_pdf(ndf, out, hf, ndf.eval(hf)), 4.0f * fabsf(dot3(out, hf)));
-      }
       // float(p / (4.0 * |o.h|)): float operands, one double op -> identical to the float division
-      else pdf = div_nr(vndf_pdf(ndf, out, h, D), 4.0f * fabsf(outh));
+      const float p = div_nr(vndf_pdf(ndf, out, h, D), 4.0f * fabsf(outh));
+      pdf = active ? p : 0.0f;
     }
+    else pdf = 0.0f;
   }
 
   // microfacet.h:115-141 sample: m ~ VNDF(out), direction = reflect(out, m)

@@ -104,9 +104,11 @@ def main():
     model = bbm_amd.BsdfModel(args.model)
     n = args.pairs
     dev = torch.device("cuda", torch.cuda.current_device())
+    from bbm_amd.shard import weak_range
     # this rank's shard [rank*n, (rank+1)*n) of the global batch, regenerated on device
-    din = bbm_amd.fill_directions(SEED, 0, rank * n, n, mode=0)
-    dout = bbm_amd.fill_directions(SEED, 1, rank * n, n, mode=0)
+    begin, _ = weak_range(n, rank)
+    din = bbm_amd.fill_directions(SEED, 0, begin, n, mode=0)
+    dout = bbm_amd.fill_directions(SEED, 1, begin, n, mode=0)
     rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
     pdf = torch.empty((n,), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream()

@@ -1,0 +1,135 @@
+// tests/cpp/adapter_check.cpp -- drop-in check of the C++ host adapter (backbone/hip).
+//
+// The SAME bbm::bsdfmodel<> instances (reference template API, native floatRGB backbone for the
+// per-pair CPU calls) are evaluated twice: once per pair on the CPU through the reference's own
+// eval/pdf/sample, once in batch on the GPU through bbm::hip::{eval_pdf, sample}.  Prints one JSON
+// line per model; exit code 1 if any model misses the parity bar.
+//
+// Built in the build container by tests/cpp/Makefile (needs /root/reference headers at compile
+// time only); the binary runs on the GPU box.
+#include "bbm/bbm_core.h"
+#include "bsdfmodel/scaledmodel.h"
+#include "bsdfmodel/microfacet.h"
+#include "bsdfmodel/lambertian.h"
+#include "bsdfmodel/cooktorrance.h"
+#include "bsdfmodel/cooktorrancewalter.h"
+#include "bsdfmodel/ggx.h"
+#include "bsdfmodel/ashikhminshirley.h"
+#include "bsdfmodel/lowmicrofacet.h"
+#include "bsdfmodel/low.h"
+#include "bbm_hip/batch.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#define HIPCHECK(x) do { hipError_t e_ = (x); if(e_ != hipSuccess) { std::fprintf(stderr, "HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); std::exit(2); } } while(0)
+
+struct dev_buf
+{
+  float* p = nullptr;
+  explicit dev_buf(size_t n) { HIPCHECK(hipMalloc(&p, n * sizeof(float))); }
+  dev_buf(const dev_buf&) = delete;
+  dev_buf& operator=(const dev_buf&) = delete;
+  dev_buf(dev_buf&& o) noexcept : p(o.p) { o.p = nullptr; }
+  ~dev_buf() { if(p) hipFree(p); }
+};
+
+static void upload(dev_buf& d, const std::vector<float>& h) { HIPCHECK(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice)); }
+static std::vector<float> download(const dev_buf& d, size_t n) { std::vector<float> h(n); HIPCHECK(hipMemcpy(h.data(), d.p, n * sizeof(float), hipMemcpyDeviceToHost)); return h; }
+
+static double relerr(double a, double b)
+{
+  if(a == b || (std::isnan(a) && std::isnan(b))) return 0;
+  return std::fabs(a - b) / std::max(std::fabs(b), 1e-30);
+}
+
+template<typename MODEL>
+static bool check_model(const MODEL& model, size_t n, unsigned seed)
+{
+  using Vec3d = typename MODEL::Vec3d;
+  using Vec2d = typename MODEL::Vec2d;
+  std::mt19937 rng(seed);
+  std::uniform_real_distribution<float> u(0.0f, 1.0f);
+  std::vector<float> h[8];
+  for(auto& v : h) v.resize(n);
+  for(size_t i = 0; i < n; ++i)
+    for(int k = 0; k < 2; ++k)
+    {
+      float z = 2.0f * u(rng) - 1.0f, phi = 6.2831853f * u(rng), s = std::sqrt(std::max(1.0f - z * z, 0.0f));
+      h[3 * k + 0][i] = s * std::cos(phi); h[3 * k + 1][i] = s * std::sin(phi); h[3 * k + 2][i] = z;
+    }
+  for(size_t i = 0; i < n; ++i) { h[6][i] = u(rng); h[7][i] = u(rng); }
+  std::vector<dev_buf> d;
+  d.reserve(8);
+  for(int k = 0; k < 8; ++k) { d.emplace_back(n); upload(d.back(), h[k]); }
+  dev_buf r(n), g(n), b(n), pdf(n), sx(n), sy(n), sz(n), spdf(n), sflag(n);
+  bbm::hip::soa3 in{d[0].p, d[1].p, d[2].p}, out{d[3].p, d[4].p, d[5].p};
+  bbm::hip::eval_pdf(model, in, out, n, {r.p, g.p, b.p}, pdf.p);
+  bbm::hip::sample(model, out, d[6].p, d[7].p, n, {sx.p, sy.p, sz.p}, spdf.p, reinterpret_cast<uint32_t*>(sflag.p));
+  HIPCHECK(hipDeviceSynchronize());
+  auto R = download(r, n), G = download(g, n), B = download(b, n), P = download(pdf, n);
+  auto SX = download(sx, n), SY = download(sy, n), SZ = download(sz, n), SP = download(spdf, n);
+  std::vector<uint32_t> SF(n);
+  HIPCHECK(hipMemcpy(SF.data(), sflag.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+
+  double peak = 0, ppeak = 0;
+  std::vector<float> ce(3 * n), cp(n);
+  for(size_t i = 0; i < n; ++i)
+  {
+    Vec3d vin(h[0][i], h[1][i], h[2][i]), vout(h[3][i], h[4][i], h[5][i]);
+    auto e = model.eval(vin, vout);
+    ce[3 * i] = e[0]; ce[3 * i + 1] = e[1]; ce[3 * i + 2] = e[2];
+    cp[i] = model.pdf(vin, vout);
+    if(std::isfinite(e[0])) peak = std::max(peak, std::fabs(double(e[0])));
+    if(std::isfinite(cp[i])) ppeak = std::max(ppeak, std::fabs(double(cp[i])));
+  }
+  size_t bad = 0, bad_flag = 0;
+  double worst = 0;
+  for(size_t i = 0; i < n; ++i)
+  {
+    const float got[4] = {R[i], G[i], B[i], P[i]};
+    const float ref[4] = {ce[3 * i], ce[3 * i + 1], ce[3 * i + 2], cp[i]};
+    for(int k = 0; k < 4; ++k)
+    {
+      const double floor = 1e-6 * (k < 3 ? peak : ppeak);
+      const double d = std::fabs(double(got[k]) - double(ref[k]));
+      if(!(got[k] == ref[k] || (std::isnan(got[k]) && std::isnan(ref[k])) || d <= 1e-5 * std::fabs(double(ref[k])) + floor)) ++bad;
+      if(std::fabs(ref[k]) > floor) worst = std::max(worst, relerr(got[k], ref[k]));
+    }
+    // sample: same flag; pdf of the GPU direction equals the CPU model's pdf at that direction
+    Vec3d vout(h[3][i], h[4][i], h[5][i]);
+    auto s = model.sample(vout, Vec2d(h[6][i], h[7][i]));
+    if(uint32_t(s.flag) != SF[i]) ++bad_flag;
+    Vec3d sd(SX[i], SY[i], SZ[i]);
+    float pref = model.pdf(sd, vout);
+    const double d = std::fabs(double(SP[i]) - double(pref));
+    if(!(SP[i] == pref || d <= 1e-5 * std::fabs(double(pref)) + 1e-6 * ppeak)) ++bad;
+  }
+  const bool ok = bad == 0 && bad_flag == 0;
+  std::printf("{\"model\": \"%s\", \"n\": %zu, \"violations\": %zu, \"flag_mismatch\": %zu, \"max_rel_err\": %.3e, \"ok\": %s}\n",
+              bbm::toString(model).c_str(), n, bad, bad_flag, worst, ok ? "true" : "false");
+  return ok;
+}
+
+int main()
+{
+  const size_t n = 1 << 18;
+  bool ok = true;
+  bbm::cooktorrance<bbm::floatRGB> ct;
+  ok &= check_model(ct, n, 1);
+  bbm::cooktorrance<bbm::floatRGB> ct2;
+  {
+    auto p = bbm::parameter_values(ct2);
+    p[0] = 0.2f; p[1] = 0.4f; p[2] = 0.6f; p[3] = 0.35f; p[4] = 2.1f;
+  }
+  ok &= check_model(ct2, n, 2);
+  ok &= check_model(bbm::ggx<bbm::floatRGB>(), n, 3);
+  ok &= check_model(bbm::lambertian<bbm::floatRGB>(), n, 4);
+  ok &= check_model(bbm::cooktorrancewalter<bbm::floatRGB>(), n, 5);
+  ok &= check_model(bbm::lowcooktorrance<bbm::floatRGB>(), n, 6);
+  return ok ? 0 : 1;
+}

@@ -174,6 +174,9 @@ def test_errors_raise(bbm):
         m.eval_pdf(d.double(), d)
 
 
+DIR_TOL_MAX = 1e-3
+
+
 def _gpu_sample(model, sout, sxi, **kw):
     s = model.sample(_dev(sout), _dev(sxi), **kw)
     torch.cuda.synchronize()
@@ -181,8 +184,16 @@ def _gpu_sample(model, sout, sxi, **kw):
 
 
 def test_sample_matches_reference_golden(bbm):
-    """sample(out, xi) -> (direction, pdf, flag) vs the reference's own samples.  Directions are
-    unit vectors: |d_gpu - d_ref| <= 1e-5 per component; pdf under the eval/pdf tolerance."""
+    """sample(out, xi) -> (direction, pdf, flag) vs the reference's own samples.
+
+    Directions are unit vectors compared per component.  Beckmann VNDF sampling inverts the slope
+    CDF with three Newton steps on erfinv (ndf/beckmann.h:92-110); at clamped xi (0.9999999) and a
+    grazing view it is ill-conditioned: swapping glibc's erff for a 1-ulp-different erf in the C
+    restatement alone moves the direction by 1.09e-5 (tests/golden CookTorrance set 2, sample 666).
+    The same edge cases with a rougher lobe reach ~5e-5.  The bar is therefore: |d_gpu - d_ref| <=
+    1e-6 on >= 99% of samples and <= 1e-3 everywhere (a wrong formula moves directions by O(0.1)),
+    flags identical, and the pdf of every GPU sample equal (1e-5) to the reference pdf evaluated at
+    that GPU direction."""
     stats = {}
     for name in _gpu_models(bbm):
         g = ou.golden_model(name)
@@ -193,13 +204,15 @@ def test_sample_matches_reference_golden(bbm):
             ref = g[f"sample{si}"]
             assert np.array_equal(flag.astype(np.uint8), g[f"sflag{si}"]), f"{name}[{si}] flags"
             derr = np.abs(got[:3].astype(np.float64) - ref[:3])
-            assert np.nanmax(derr) <= 1e-5, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
+            assert np.nanmax(derr) <= DIR_TOL_MAX, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
+            assert np.mean(derr.max(0) > 1e-6) <= 0.01, f"{name}[{si}] too many directions off by > 1e-6"
             # the pdf of a sample is pdf(direction): for a sharp lobe a 1-ulp direction difference
             # moves it by more than 1e-5, so it is checked at the GPU's own direction (reference
             # pdf via the bit-exact restatement) and the raw difference is reported
             pref = ou.port_eval_pdf(name, g[f"params{si}"], got[:3], INP["sout"])[3]
             st = _assert_parity(got[3:], pref[None], f"{name}[{si}] pdf(dir)")
             st["max_dir_abs_err"] = float(np.nanmax(derr))
+            st["frac_dir_within_1e-6"] = float(np.mean(derr.max(0) <= 1e-6))
             st["raw_pdf_max_rel"] = float(ou.rel_err(got[3], ref[3]).max())
             stats[f"{name}[{si}]"] = st
     _report("sample", stats)
@@ -219,6 +232,24 @@ def test_sample_large_batch_vs_port(bbm):
         got = np.concatenate([s.direction.cpu().numpy(), s.pdf.cpu().numpy()[None]], 0)
         ref, flag = ou.port_sample(name, m.parameter_values(), hout, hxi, nthreads=8)
         assert np.array_equal(s.flag.cpu().numpy().astype(np.uint32), flag), name
-        assert np.nanmax(np.abs(got[:3].astype(np.float64) - ref[:3])) <= 1e-5, name
+        derr = np.abs(got[:3].astype(np.float64) - ref[:3])
+        assert np.nanmax(derr) <= DIR_TOL_MAX, name
+        assert np.mean(derr.max(0) > 1e-6) <= 0.01, name
         pref = ou.port_eval_pdf(name, m.parameter_values(), got[:3], hout, nthreads=8)[3]
         _assert_parity(got[3:], pref[None], f"{name} pdf(dir)")
+
+
+def test_cpp_adapter_drop_in(bbm):
+    """backbone/hip C++ adapter: the same bbm::bsdfmodel<> instances (reference template API) on the
+    CPU (native backbone) and through bbm::hip::{eval_pdf, sample} on the GPU (tests/cpp)."""
+    import os
+    import subprocess
+    exe = os.path.join(ou.ROOT, "tests", "cpp", "_build", "adapter_check")
+    if not os.path.exists(exe):
+        pytest.skip("tests/cpp/_build/adapter_check not built (needs the reference headers at build time)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    os.makedirs(os.path.join(ou.ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ou.ROOT, "gpurun_out", "adapter_check.jsonl"), "w") as f:
+        f.write(r.stdout)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
