@@ -124,6 +124,62 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
   }
 }
 
+// Software-pipelined grid-stride variant: the six 16-byte loads of the thread's NEXT quad are
+// issued before the current quad is computed, so every wave keeps HBM reads in flight while its
+// VALU work runs (the plain kernel only overlaps load and compute across different waves).
+template<class Model, int MODE, bool MASK, bool NT>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_pipe(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t < n4)
+  {
+    float4 c[6];
+    uint32_t cm = 0x01010101u;
+    c[0] = ld4<NT>(a.ix, t); c[1] = ld4<NT>(a.iy, t); c[2] = ld4<NT>(a.iz, t);
+    c[3] = ld4<NT>(a.ox, t); c[4] = ld4<NT>(a.oy, t); c[5] = ld4<NT>(a.oz, t);
+    if (MASK) cm = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    for (; t < n4; t += stride)
+    {
+      const uint64_t tn = (t + stride < n4) ? t + stride : t;   // clamped: the last prefetch re-reads
+      float4 nx[6];
+      uint32_t nm = 0x01010101u;
+      nx[0] = ld4<NT>(a.ix, tn); nx[1] = ld4<NT>(a.iy, tn); nx[2] = ld4<NT>(a.iz, tn);
+      nx[3] = ld4<NT>(a.ox, tn); nx[4] = ld4<NT>(a.oy, tn); nx[5] = ld4<NT>(a.oz, tn);
+      if (MASK) nm = reinterpret_cast<const uint32_t*>(a.mask)[tn];
+      const float inx[4] = {c[0].x, c[0].y, c[0].z, c[0].w}, iny[4] = {c[1].x, c[1].y, c[1].z, c[1].w};
+      const float inz[4] = {c[2].x, c[2].y, c[2].z, c[2].w}, onx[4] = {c[3].x, c[3].y, c[3].z, c[3].w};
+      const float ony[4] = {c[4].x, c[4].y, c[4].z, c[4].w}, onz[4] = {c[5].x, c[5].y, c[5].z, c[5].w};
+      float r[4], g[4], b[4], p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        float rgb[3];
+        const uint32_t comp = ((cm >> (8 * j)) & 0xffu) ? a.component : 0u;
+        m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
+        r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
+      }
+      if (MODE & kModeEval)
+      {
+        st4<NT>(a.r, t, r[0], r[1], r[2], r[3]);
+        st4<NT>(a.g, t, g[0], g[1], g[2], g[3]);
+        st4<NT>(a.b, t, b[0], b[1], b[2], b[3]);
+      }
+      if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) c[k] = nx[k];
+      cm = nm;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
 // Scalar path for unaligned arrays.
 template<class Model, int MODE, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
@@ -141,6 +197,16 @@ uint64_t max_blocks()
     const char* e = std::getenv("BBM_HIP_MAX_BLOCKS");
     const long long x = e ? std::atoll(e) : 0;
     return x > 0 ? uint64_t(x) : uint64_t(kMaxBlocks);
+  }();
+  return v;
+}
+
+// Software-pipelined grid-stride kernel (BBM_HIP_PIPE=1; tuning experiments).
+bool use_pipe()
+{
+  static const bool v = [] {
+    const char* e = std::getenv("BBM_HIP_PIPE");
+    return e ? std::atoi(e) != 0 : false;
   }();
   return v;
 }
@@ -239,7 +305,8 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
   uint64_t blocks = (units + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
-  if (vec && use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  if (vec && use_pipe()) hipLaunchKernelGGL((k_eval_pdf_pipe<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec && use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, false>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();

@@ -10,7 +10,7 @@ cat gpurun_out/adapter_check.jsonl 2>/dev/null
 for round in 1 2; do
 for V in ${AB_VARIANTS:-"BBM_HIP_NT=1"}; do
   for M in ${BENCH_MODELS:-CookTorrance}; do
-  env $V timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu --model $M > gpurun_out/v.json 2>gpurun_out/v.err || { echo "variant $V failed"; tail gpurun_out/v.err; exit 1; }
+  env $(echo $V | tr "," " ") timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu --model $M > gpurun_out/v.json 2>gpurun_out/v.err || { echo "variant $V failed"; tail gpurun_out/v.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/v.json'));print('r$round $M $V', '%.4e'%d['value'], '%.1f GB/s'%d['roofline']['achieved'], 'frac %.3f'%d['roofline']['frac'], '%.3f ms'%d['roofline']['kernel_ms'])"
   done
 done
