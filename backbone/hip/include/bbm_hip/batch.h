@@ -79,6 +79,27 @@ namespace bbm {
         if constexpr (std::is_same_v<M, bbm::cooktorrancewalter<C>>) return "CookTorranceWalter";
         else
 #endif
+#ifdef _BBM_COOKTORRANCEHEITZ_H_
+        if constexpr (std::is_same_v<M, bbm::cooktorranceheitz<C>>) return "CookTorranceHeitz";
+        else
+#endif
+#ifdef _BBM_GGX_HEITZ_H_
+        if constexpr (std::is_same_v<M, bbm::ggxheitz<C>>) return "GGXHeitz";
+        else
+#endif
+#ifdef _BBM_PHONG_WALTER_H_
+        if constexpr (std::is_same_v<M, bbm::phongwalter<C>>) return "PhongWalter";
+        else
+#endif
+#ifdef _BBM_RIBARDIERE_H_
+        if constexpr (std::is_same_v<M, bbm::ribardiere<C>>) return "Ribardiere";
+        else if constexpr (std::is_same_v<M, bbm::ribardiereanisotropic<C>>) return "RibardiereAnisotropic";
+        else
+#endif
+#ifdef _BBM_NGAN_H_
+        if constexpr (std::is_same_v<M, bbm::ngancooktorrance<C>>) return "NganCookTorrance";
+        else
+#endif
         static_assert(dependent_false<M>::value, "this bsdfmodel composition has no HIP kernel (see DESIGN.md)");
         return nullptr;
       }

@@ -81,8 +81,16 @@ __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, floa
   else reinterpret_cast<float4*>(p)[t] = make_float4(a, b, c, d);
 }
 
+#ifndef BBM_HIP_SGPR_LIMIT
+#define BBM_HIP_KERNEL_ATTR
+#else
+// Cap the SGPR budget: 256-thread workgroups are admitted per CU only up to
+// floor(800 / (ceil(sgpr/16)*16 + 16)) (MI355X_MICROARCH.md, Residency) -- 98 SGPRs = 6 per CU.
+#define BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_num_sgpr(BBM_HIP_SGPR_LIMIT)))
+#endif
+
 template<class Model, int MODE, bool MASK, bool NT>
-__global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
+__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v4(EvalArgs a)
 {
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
@@ -117,6 +125,65 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v4(EvalArgs a)
     if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
   }
   // tail
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+// Eight pairs per thread: two quads, each a fully coalesced 1 KiB wave access (quad t and quad
+// t + 64 within the wave's 128-quad tile).  More independent work per wave for the scheduler.
+template<class Model, int MODE, bool MASK, bool NT>
+__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v8(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t stride = uint64_t(gridDim.x) * (2 * kBlock);
+  for (uint64_t base = uint64_t(blockIdx.x) * (2 * kBlock) + wave * 128; base < n4; base += stride)
+  {
+    uint64_t tq[2] = {base + lane, base + 64 + lane};
+    float4 c[2][6];
+    uint32_t cm[2] = {0x01010101u, 0x01010101u};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      const uint64_t t = tq[u] < n4 ? tq[u] : n4 - 1;
+      c[u][0] = ld4<NT>(a.ix, t); c[u][1] = ld4<NT>(a.iy, t); c[u][2] = ld4<NT>(a.iz, t);
+      c[u][3] = ld4<NT>(a.ox, t); c[u][4] = ld4<NT>(a.oy, t); c[u][5] = ld4<NT>(a.oz, t);
+      if (MASK) cm[u] = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    }
+    float r[2][4], g[2][4], b[2][4], p[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      const float inx[4] = {c[u][0].x, c[u][0].y, c[u][0].z, c[u][0].w}, iny[4] = {c[u][1].x, c[u][1].y, c[u][1].z, c[u][1].w};
+      const float inz[4] = {c[u][2].x, c[u][2].y, c[u][2].z, c[u][2].w}, onx[4] = {c[u][3].x, c[u][3].y, c[u][3].z, c[u][3].w};
+      const float ony[4] = {c[u][4].x, c[u][4].y, c[u][4].z, c[u][4].w}, onz[4] = {c[u][5].x, c[u][5].y, c[u][5].z, c[u][5].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        float rgb[3];
+        const uint32_t comp = ((cm[u] >> (8 * j)) & 0xffu) ? a.component : 0u;
+        m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[u][j]);
+        r[u][j] = rgb[0]; g[u][j] = rgb[1]; b[u][j] = rgb[2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      if (tq[u] >= n4) continue;
+      const uint64_t t = tq[u];
+      if (MODE & kModeEval)
+      {
+        st4<NT>(a.r, t, r[u][0], r[u][1], r[u][2], r[u][3]);
+        st4<NT>(a.g, t, g[u][0], g[u][1], g[u][2], g[u][3]);
+        st4<NT>(a.b, t, b[u][0], b[u][1], b[u][2], b[u][3]);
+      }
+      if (MODE & kModePdf) st4<NT>(a.pdf, t, p[u][0], p[u][1], p[u][2], p[u][3]);
+    }
+  }
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
   {
     const uint64_t i = (n4 << 2) + threadIdx.x;
@@ -197,6 +264,16 @@ uint64_t max_blocks()
     const char* e = std::getenv("BBM_HIP_MAX_BLOCKS");
     const long long x = e ? std::atoll(e) : 0;
     return x > 0 ? uint64_t(x) : uint64_t(kMaxBlocks);
+  }();
+  return v;
+}
+
+// Pairs per thread of the vector kernel (BBM_HIP_PPT=8 selects k_eval_pdf_v8; tuning experiments).
+int pairs_per_thread()
+{
+  static const int v = [] {
+    const char* e = std::getenv("BBM_HIP_PPT");
+    return (e && std::atoi(e) == 8) ? 8 : 4;
   }();
   return v;
 }
@@ -302,10 +379,13 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
   if (MODE & kModeEval) vec = vec && aligned16(a.r) && aligned16(a.g) && aligned16(a.b);
   if (MODE & kModePdf) vec = vec && aligned16(a.pdf);
   const uint64_t units = vec ? (a.n >> 2) : a.n;
-  uint64_t blocks = (units + kBlock - 1) / kBlock;
+  const uint64_t per_block = (vec && pairs_per_thread() == 8) ? 2 * kBlock : kBlock;
+  uint64_t blocks = (units + per_block - 1) / per_block;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
-  if (vec && use_pipe()) hipLaunchKernelGGL((k_eval_pdf_pipe<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  if (vec && pairs_per_thread() == 8)
+    hipLaunchKernelGGL((k_eval_pdf_v8<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec && use_pipe()) hipLaunchKernelGGL((k_eval_pdf_pipe<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else if (vec && use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, false>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
@@ -371,6 +451,13 @@ using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, N
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                        // bsdfmodel/ggx.h:27-33
 using CookTorranceWalterM = Microfacet<Beckmann<false, true>, Uncorrelated, FresnelCook, Norm::Walter, true>;  // bsdfmodel/cooktorrancewalter.h:32-38
 
+using CookTorranceHeitzM = Microfacet<Beckmann<true, true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;   // bsdfmodel/cooktorranceheitz.h:33-39
+using GGXHeitzM = Microfacet<GGX<true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;                     // bsdfmodel/ggxheitz.h:28-34
+using NganCookTorranceM = Microfacet<Beckmann<false, true>, VGroove, FresnelSchlick, Norm::Cook, true>;         // bsdfmodel/ngan.h:141-147
+using PhongWalterM = Microfacet<PhongNdf, Uncorrelated, FresnelCook, Norm::Walter, true>;                         // bsdfmodel/phongwalter.h:27-33
+using RibardiereM = Microfacet<StudentT<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                   // bsdfmodel/ribardiere.h:28-34
+using RibardiereAnisoM = Microfacet<StudentT<true>, Uncorrelated, FresnelCook, Norm::Walter, true>;              // bsdfmodel/ribardiere.h:46-52
+
 constexpr float kFMax = 3.4028234663852886e+38f;
 
 // Defaults and bounds: bsdf_attribute.h:73-94 (scale 0.5 in [0,1], roughness 0.1 in [0,1] as
@@ -387,6 +474,18 @@ const ModelEntry kModels[] = {
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
   {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
+  {"CookTorranceHeitz", 6, kFlagSpecular, &launch_eval_pdf<CookTorranceHeitzM>, &launch_sample<CookTorranceHeitzM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}},
+  {"GGXHeitz", 6, kFlagSpecular, &launch_eval_pdf<GGXHeitzM>, &launch_sample<GGXHeitzM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}},
+  {"NganCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<NganCookTorranceM>, &launch_sample<NganCookTorranceM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, 0}, {1, 1, 1, 1, 1}},
+  {"PhongWalter", 5, kFlagSpecular, &launch_eval_pdf<PhongWalterM>, &launch_sample<PhongWalterM>,
+   {0.5f, 0.5f, 0.5f, 32.0f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, kFMax, 5}},
+  {"Ribardiere", 6, kFlagSpecular, &launch_eval_pdf<RibardiereM>, &launch_sample<RibardiereM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 40, 5}},
+  {"RibardiereAnisotropic", 7, kFlagSpecular, &launch_eval_pdf<RibardiereAnisoM>, &launch_sample<RibardiereAnisoM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 1, 40, 5}},
 };
 constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
 

@@ -12,6 +12,9 @@ namespace bbmhip {
 
 // ------------------------------------------------------------------------------------- NDFs
 
+template<class NDF>
+__device__ __forceinline__ float vndf_pdf(const NDF& ndf, v3 view, v3 m, float D);
+
 // ndf::beckmann<CONF, Symmetry, Normalize> (include/ndf/beckmann.h:40-213)
 template<bool Aniso, bool Normalize>
 struct Beckmann
@@ -69,6 +72,8 @@ struct Beckmann
     const float u1 = ((0.0f + s * s0) + c * s1) * av;
     return normalize3(mk3(-u0, -u1, 1.0f));
   }
+
+  __device__ __forceinline__ float pdf(v3 view, v3 m, float D) const { return vndf_pdf(*this, view, m, D); }
 };
 
 // ndf::ggx<CONF, Symmetry> (include/ndf/ggx.h:37-196)
@@ -119,9 +124,131 @@ struct GGX
                      (T1.z * P1 + T2.z * P2) + vs.z * sq);
     return normalize3(mk3(n.x * au, n.y * av, float(fmax(0.0, double(n.z)))));
   }
+
+  __device__ __forceinline__ float pdf(v3 view, v3 m, float D) const { return vndf_pdf(*this, view, m, D); }
 };
 
-// ndf pdf shared by Beckmann/GGX VNDF sampling (beckmann.h:149-170, ggx.h:142-163):
+// ndf::phong (include/ndf/phong.h:31-140): D = (s + 2) / (2 pi) cos^s; pdf = D |cos|; Walter's
+// G1 rational with a = sqrt(0.5 s + 1) / tan (double); sampling cos = xi0^(1/(s+2)) (double pow)
+struct PhongNdf
+{
+  static constexpr int kParams = 1;
+  float sharpness;
+  __device__ explicit PhongNdf(const float* p) : sharpness(p[0]) {}
+
+  __device__ __forceinline__ float eval(v3 h) const
+  {
+    const float normalization = div_nr(sharpness + 2, float(2.0f * kPiD));
+    const float D = powf(h.z, sharpness) * normalization;
+    return (h.z > 0) ? D : 0.0f;
+  }
+  __device__ __forceinline__ float G1(v3 v, v3 m) const
+  {
+    const bool mask = (v.z > 0) && (dot3(v, m) > 0);
+    const float a = float(sqrt(0.5 * sharpness + 1) / double(tan_theta(v)));
+    const double ad = a;
+    const float g = f_div_d(3.535 * ad + 2.181 * ad * ad, 1 + 2.276 * ad + 2.577 * ad * ad);
+    return mask ? ((a < 1.6) ? g : 1.0f) : 0.0f;
+  }
+  __device__ __forceinline__ float pdf(v3, v3 m, float D) const { return (m.z > 0) ? D * fabsf(m.z) : 0.0f; }
+  __device__ __forceinline__ v3 sample(v3, float xi0, float xi1) const
+  {
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
+    const float cosT = float(pow(double(xi0), 1.0 / (sharpness + 2)));
+    const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
+    float sp, cp;
+    sincosf(xi1 * float(2.0f * kPiD), &sp, &cp);
+    return mk3(cp * sinT, sp * sinT, cosT);
+  }
+};
+
+// ndf::studentt (include/ndf/studentt.h:34-195), Ribardiere et al. 2017; G1 via the paper's
+// rational fits F21..F24 (float results of double-promoted expressions) and tgamma.
+template<bool Aniso>
+struct StudentT
+{
+  static constexpr int kParams = (Aniso ? 2 : 1) + 1;
+  float au, av, gamma;
+  __device__ explicit StudentT(const float* p) : au(p[0]), av(Aniso ? p[1] : p[0]), gamma(p[Aniso ? 2 : 1]) {}
+
+  __device__ __forceinline__ float eval(v3 h) const
+  {
+    const float alpha2 = (1.0f * au) * av;
+    const float z2 = h.z * h.z;
+    const float normalization = kPiF * alpha2 * (z2 * z2);       // pow(cos, 4): powf(x, 4) = (x^2)^2 exactly rounded here
+    const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
+    const float den = float(pow(1.0 + div_nr(sn, (gamma - 1) * pow2f(h.z)), double(gamma)));
+    const float D = div_nr(1.0f, normalization * den);
+    return (h.z > 0) ? D : 0.0f;
+  }
+
+  __device__ __forceinline__ static float F21(float z)
+  {
+    const float z2 = z * z, z3 = z2 * z;
+    const float num = float(1.066 * z + 2.655 * z2 + 4.892 * z3);
+    const float den = float(1.038 + 2.969 * z + 4.305 * z2 + 4.418 * z3);
+    return div_nr(num, den);
+  }
+  __device__ __forceinline__ static float F22(float g)
+  {
+    const float g2 = g * g, g3 = g2 * g;
+    return div_nr(float(14.402 - 27.145 * g + 20.574 * g2 - 2.745 * g3), float(-30.612 + 86.567 * g - 84.341 * g2 + 29.938 * g3));
+  }
+  __device__ __forceinline__ static float F23(float g)
+  {
+    const float g2 = g * g, g3 = g2 * g;
+    return div_nr(float(-129.404 + 324.987 * g - 299.305 * g2 + 93.268 * g3), float(-92.609 + 256.006 * g - 245.663 * g2 + 86.064 * g3));
+  }
+  __device__ __forceinline__ static float F24(float z)
+  {
+    const float z2 = z * z, z3 = z2 * z;
+    return div_nr(float(6.537 + 6.074 * z - 0.623 * z2 + 5.223 * z3), float(6.538 + 6.103 * z - 3.218 * z2 + 6.347 * z3));
+  }
+
+  // studentt.h:128-156
+  __device__ __forceinline__ float G1(v3 v, v3 m) const
+  {
+    const bool mask = (v.z > 0) && (dot3(v, m) > 0);
+    const bool normal_mask = v.z < 1.0 - kEpsF;
+    const float z = v.z * div_nr(1.0f, sqrtf(sqnorm2(v.x * au, v.y * av)));
+    const float S1 = float(pow(double((gamma - 1) + z * z), 3.0 / 2.0 - gamma) / z);
+    const float S2 = F21(z) * (F22(gamma) + F23(gamma) * F24(z));
+    const float S1_scale = div_nr(powf(gamma - 1, gamma), 2 * gamma - 3);
+    const double lam = tgamma(gamma - 0.5) / double(tgammaf(gamma)) * kInvSqrtPiF *
+                       double(S1_scale * S1 + sqrtf(gamma - 1) * S2) - 0.5;
+    const float lambda = normal_mask ? float(lam) : 0.0f;
+    const float g = float(1.0 / (1.0 + lambda));
+    return mask ? (normal_mask ? g : 1.0f) : 0.0f;
+  }
+
+  __device__ __forceinline__ float pdf(v3, v3 m, float D) const
+  {
+    const float p = D * m.z;
+    return ((m.z > 0) && (p > 0)) ? p : 0.0f;
+  }
+
+  // studentt.h:64-90
+  __device__ __forceinline__ v3 sample(v3, float xi0, float xi1) const
+  {
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
+    float sp, cp;
+    sincosf(float(2.0f * kPiD) * xi0, &sp, &cp);
+    float normalization;
+    if (Aniso)
+    {
+      normalization = div_nr(1.0f, sqnorm2(div_nr(cp, au), div_nr(sp, av)));
+      const v3 cs = normalize3(mk3(cp * au, sp * av, 0.0f));
+      cp = cs.x; sp = cs.y;
+    }
+    else normalization = au * au;
+    const float tan2 = float((pow(double(xi1), 1.0 / (1.0 - gamma)) - 1) * (gamma - 1) * normalization);
+    const float cosT = float(1.0 / sqrt(1.0 + tan2));
+    const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
+    return mk3(cp * sinT, sp * sinT, cosT);
+  }
+};
+
+// ndf pdf shared by Beckmann/GGX VNDF sampling (declared before use by the NDF structs below) (beckmann.h:149-170, ggx.h:142-163):
 // D(m) * G1(view, m) * |view.m| / cos(view), masked to pdf > 0.  D(m) is passed in (already
 // computed by eval on the same halfway vector).
 template<class NDF>
@@ -167,6 +294,20 @@ struct Uncorrelated
   }
 };
 
+// maskingshadowing::heightcorrelated (include/maskingshadowing/heightcorrelated.h:30-54), Heitz 2014 Eq. 99
+struct HeightCorrelated
+{
+  template<class NDF>
+  __device__ __forceinline__ static float eval(const NDF& ndf, v3 in, v3 out, v3 m, float inm, float outm)
+  {
+    const float gi = ndf.G1(in, m), go = ndf.G1(out, m);
+    const float gio = gi * go;
+    const float denom = gi + go - gio;
+    const float g = div_nr(gio, denom);
+    return ((inm > 0) && (outm > 0) && (denom > kEpsF)) ? g : 0.0f;
+  }
+};
+
 // ---------------------------------------------------------------------------- fresnel
 
 // fresnel::cook with a scalar ior (include/bbm/fresnel_cook.h:41-56)
@@ -181,6 +322,22 @@ struct FresnelCook
     const float a = div_nr(g - c, g + c);
     const float b = div_nr(c * (g + c) - 1.0f, c * (g - c) + 1.0f);
     return fmaxf(0.5f * (a * a) * (1.0f + b * b), 0.0f);   // bbm::max(x, 0.0): fmax in double == fmaxf here
+  }
+};
+
+// fresnel::schlick with a reflectance parameter (include/bbm/fresnel_schlick.h:42-53):
+// R0 + (1 - R0) * pow(1 - cos, 5.0) in double (pow(x, 5.0) of a float x: x^2 exact, then two
+// rounded products -- within 1.5 double ulp, below the final float rounding)
+struct FresnelSchlick
+{
+  static constexpr int kParams = 1;
+  float r0;
+  __device__ explicit FresnelSchlick(const float* p) : r0(p[0]) {}
+  __device__ __forceinline__ float eval(float c) const
+  {
+    const double x = double(1.0f - c);
+    const double x2 = x * x;
+    return float(r0 + double(1.0f - r0) * (x2 * x2 * x));
   }
 };
 
@@ -262,7 +419,7 @@ struct Microfacet
     if (MODE & kModePdf)
     {
       // float(p / (4.0 * |o.h|)): float operands, one double op -> identical to the float division
-      const float p = div_nr(vndf_pdf(ndf, out, h, D), 4.0f * fabsf(outh));
+      const float p = div_nr(ndf.pdf(out, h, D), 4.0f * fabsf(outh));
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;

@@ -93,6 +93,34 @@ def port_sample(name, params, dout, xi, component=3, unit=0, nthreads=1):
     return _sample(port().bbmport_sample, name, params, dout, xi, component, unit, nthreads)
 
 
+def ref_sample(name, params, dout, xi, component=3, unit=0, nthreads=1):
+    lib = ref()
+    if lib is None:
+        return None
+    return _sample(lib.bbmref_sample, name, params, dout, xi, component, unit, nthreads)
+
+
+def oracle_models():
+    """Models a CPU checker can evaluate on arbitrary inputs: the reference shim if it is present
+    (prebuilt in the build container, travels with the tree), else the C restatement."""
+    lib = ref()
+    if lib is not None:
+        return [lib.bbmref_model_name(i).decode() for i in range(lib.bbmref_num_models())]
+    return port_models()
+
+
+def oracle_eval_pdf(name, params, din, dout, component=3, unit=0, nthreads=1):
+    if ref() is not None:
+        return ref_eval_pdf(name, params, din, dout, component, unit, nthreads)
+    return port_eval_pdf(name, params, din, dout, component, unit, nthreads)
+
+
+def oracle_sample(name, params, dout, xi, component=3, unit=0, nthreads=1):
+    if ref() is not None:
+        return ref_sample(name, params, dout, xi, component, unit, nthreads)
+    return port_sample(name, params, dout, xi, component, unit, nthreads)
+
+
 # ------------------------------------------------------------------------------ golden
 
 def golden_meta():

@@ -108,19 +108,20 @@ def test_eval_pdf_fused_equals_separate_calls(bbm):
         assert torch.equal(rgb, rgb2) and torch.equal(pdf, pdf2), name
 
 
-def test_large_batch_vs_port(bbm):
-    """1M pairs per model against the C restatement (which is bit-exact vs the reference)."""
+def test_large_batch_vs_oracle(bbm):
+    """1M pairs per model against the reference itself (prebuilt oracle/_ref shim) or, where it
+    is absent, the C restatement (bit-exact vs the reference on the golden vectors)."""
     n = 1 << 20
     din = bbm.fill_directions(0xBB5EED, 0, 0, n, mode=0)
     dout = bbm.fill_directions(0xBB5EED, 1, 0, n, mode=1)
     hin, hout = din.cpu().numpy(), dout.cpu().numpy()
     stats = {}
     for name in _gpu_models(bbm):
-        if name not in ou.port_models():
+        if name not in ou.oracle_models():
             continue
         m = bbm.BsdfModel(name)
         got = _gpu_evalpdf(m, hin, hout)
-        ref = ou.port_eval_pdf(name, m.parameter_values(), hin, hout, nthreads=8)
+        ref = ou.oracle_eval_pdf(name, m.parameter_values(), hin, hout, nthreads=8)
         stats[name] = _assert_parity(got, ref, name)
     _report("large", stats)
 
@@ -209,7 +210,7 @@ def test_sample_matches_reference_golden(bbm):
             # the pdf of a sample is pdf(direction): for a sharp lobe a 1-ulp direction difference
             # moves it by more than 1e-5, so it is checked at the GPU's own direction (reference
             # pdf via the bit-exact restatement) and the raw difference is reported
-            pref = ou.port_eval_pdf(name, g[f"params{si}"], got[:3], INP["sout"])[3]
+            pref = ou.oracle_eval_pdf(name, g[f"params{si}"], got[:3], INP["sout"])[3]
             st = _assert_parity(got[3:], pref[None], f"{name}[{si}] pdf(dir)")
             st["max_dir_abs_err"] = float(np.nanmax(derr))
             st["frac_dir_within_1e-6"] = float(np.mean(derr.max(0) <= 1e-6))
@@ -218,24 +219,24 @@ def test_sample_matches_reference_golden(bbm):
     _report("sample", stats)
 
 
-def test_sample_large_batch_vs_port(bbm):
+def test_sample_large_batch_vs_oracle(bbm):
     n = 1 << 20
     out = bbm.fill_directions(0xBB5EED, 2, 0, n, mode=1)
     xi = torch.rand((2, n), generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")
     hout, hxi = out.cpu().numpy(), xi.cpu().numpy()
     for name in _gpu_models(bbm):
-        if name not in ou.port_models():
+        if name not in ou.oracle_models():
             continue
         m = bbm.BsdfModel(name)
         s = m.sample(out, xi)
         torch.cuda.synchronize()
         got = np.concatenate([s.direction.cpu().numpy(), s.pdf.cpu().numpy()[None]], 0)
-        ref, flag = ou.port_sample(name, m.parameter_values(), hout, hxi, nthreads=8)
+        ref, flag = ou.oracle_sample(name, m.parameter_values(), hout, hxi, nthreads=8)
         assert np.array_equal(s.flag.cpu().numpy().astype(np.uint32), flag), name
         derr = np.abs(got[:3].astype(np.float64) - ref[:3])
         assert np.nanmax(derr) <= DIR_TOL_MAX, name
         assert np.mean(derr.max(0) > 1e-6) <= 0.01, name
-        pref = ou.port_eval_pdf(name, m.parameter_values(), got[:3], hout, nthreads=8)[3]
+        pref = ou.oracle_eval_pdf(name, m.parameter_values(), got[:3], hout, nthreads=8)[3]
         _assert_parity(got[3:], pref[None], f"{name} pdf(dir)")
 
 
