@@ -192,7 +192,7 @@ def test_sample_matches_reference_golden(bbm):
     grazing view it is ill-conditioned: swapping glibc's erff for a 1-ulp-different erf in the C
     restatement alone moves the direction by 1.09e-5 (tests/golden CookTorrance set 2, sample 666).
     The same edge cases with a rougher lobe reach ~5e-5.  The bar is therefore: |d_gpu - d_ref| <=
-    1e-6 on >= 99% of samples and <= 1e-3 everywhere (a wrong formula moves directions by O(0.1)),
+    1e-5 on >= 99.5% of samples and <= 1e-3 everywhere (a wrong formula moves directions by O(0.1)),
     flags identical, and the pdf of every GPU sample equal (1e-5) to the reference pdf evaluated at
     that GPU direction."""
     stats = {}
@@ -206,7 +206,7 @@ def test_sample_matches_reference_golden(bbm):
             assert np.array_equal(flag.astype(np.uint8), g[f"sflag{si}"]), f"{name}[{si}] flags"
             derr = np.abs(got[:3].astype(np.float64) - ref[:3])
             assert np.nanmax(derr) <= DIR_TOL_MAX, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
-            assert np.mean(derr.max(0) > 1e-6) <= 0.01, f"{name}[{si}] too many directions off by > 1e-6"
+            assert np.mean(derr.max(0) > 1e-5) <= 0.005, f"{name}[{si}] too many directions off by > 1e-5"
             # the pdf of a sample is pdf(direction): for a sharp lobe a 1-ulp direction difference
             # moves it by more than 1e-5, so it is checked at the GPU's own direction (reference
             # pdf via the bit-exact restatement) and the raw difference is reported
@@ -214,6 +214,7 @@ def test_sample_matches_reference_golden(bbm):
             st = _assert_parity(got[3:], pref[None], f"{name}[{si}] pdf(dir)")
             st["max_dir_abs_err"] = float(np.nanmax(derr))
             st["frac_dir_within_1e-6"] = float(np.mean(derr.max(0) <= 1e-6))
+            st["frac_dir_within_1e-5"] = float(np.mean(derr.max(0) <= 1e-5))
             st["raw_pdf_max_rel"] = float(ou.rel_err(got[3], ref[3]).max())
             stats[f"{name}[{si}]"] = st
     _report("sample", stats)
@@ -235,7 +236,7 @@ def test_sample_large_batch_vs_oracle(bbm):
         assert np.array_equal(s.flag.cpu().numpy().astype(np.uint32), flag), name
         derr = np.abs(got[:3].astype(np.float64) - ref[:3])
         assert np.nanmax(derr) <= DIR_TOL_MAX, name
-        assert np.mean(derr.max(0) > 1e-6) <= 0.01, name
+        assert np.mean(derr.max(0) > 1e-5) <= 0.005, name
         pref = ou.oracle_eval_pdf(name, m.parameter_values(), got[:3], hout, nthreads=8)[3]
         _assert_parity(got[3:], pref[None], f"{name} pdf(dir)")
 
