@@ -98,6 +98,56 @@ namespace bbm {
 #endif
 #ifdef _BBM_NGAN_H_
         if constexpr (std::is_same_v<M, bbm::ngancooktorrance<C>>) return "NganCookTorrance";
+        else if constexpr (std::is_same_v<M, bbm::nganward<C>>) return "NganWard";
+        else if constexpr (std::is_same_v<M, bbm::nganwardduer<C>>) return "NganWardDuer";
+        else if constexpr (std::is_same_v<M, bbm::nganblinnphong<C>>) return "NganBlinnPhong";
+        else if constexpr (std::is_same_v<M, bbm::nganlafortune<C>>) return "NganLafortune";
+        else if constexpr (std::is_same_v<M, bbm::nganashikhminshirley<C>>) return "NganAshikhminShirley";
+        else
+#endif
+#ifdef _BBM_ORENNAYAR_H_
+        if constexpr (std::is_same_v<M, bbm::orennayar<C>>) return "OrenNayar";
+        else
+#endif
+#ifdef _BBM_WARD_H_
+        if constexpr (std::is_same_v<M, bbm::ward<C>>) return "Ward";
+        else
+#endif
+#ifdef _BBM_WARD_DUER_H_
+        if constexpr (std::is_same_v<M, bbm::wardduer<C>>) return "WardDuer";
+        else
+#endif
+#ifdef _BBM_WARD_DUER_GEISLER_MORODER_H_
+        if constexpr (std::is_same_v<M, bbm::wardduergeislermoroder<C>>) return "WardDuerGeislerMoroder";
+        else
+#endif
+#ifdef _BBM_PHONG_H_
+        if constexpr (std::is_same_v<M, bbm::phong<C>>) return "Phong";
+        else
+#endif
+#ifdef _BBM_LAFORTUNE_H_
+        if constexpr (std::is_same_v<M, bbm::lafortune<C>>) return "Lafortune";
+        else
+#endif
+#ifdef _BBM_ASHIKHMIN_SHIRLEY_H_
+        if constexpr (std::is_same_v<M, bbm::ashikhminshirley<C>>) return "AshikhminShirley";
+        else
+#endif
+#ifdef _BBM_ASHIKHMIN_SHIRLEY_FULL_H_
+        if constexpr (std::is_same_v<M, bbm::ashikhminshirleyfull<C>>) return "AshikhminShirleyFull";
+        else
+#endif
+#ifdef _BBM_LOW_SMOOTH_H_
+        if constexpr (std::is_same_v<M, bbm::lowsmooth<C>>) return "LowSmooth";
+        else
+#endif
+#ifdef _BBM_LOW_MICROFACET_H_
+        if constexpr (std::is_same_v<M, bbm::lowmicrofacet<C>>) return "LowMicrofacet";
+        else
+#endif
+#ifdef _BBM_LOW_FITMODELS_H_
+        if constexpr (std::is_same_v<M, bbm::lowmicrofacetfit<C>>) return "LowMicrofacetFit";
+        else if constexpr (std::is_same_v<M, bbm::lowashikhminshirley<C>>) return "LowAshikhminShirley";
         else
 #endif
         static_assert(dependent_false<M>::value, "this bsdfmodel composition has no HIP kernel (see DESIGN.md)");

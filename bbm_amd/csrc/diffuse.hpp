@@ -1,4 +1,4 @@
-// bbm_amd/csrc/diffuse.hpp -- the diffuse family (Lambertian).
+// bbm_amd/csrc/diffuse.hpp -- the diffuse family (Lambertian, Oren-Nayar).
 #pragma once
 #include "math.hpp"
 #include "microfacet.hpp"   // kMode*
@@ -40,6 +40,46 @@ struct Lambertian
     float rgb[3];
     eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
     flag = kFlagDiffuse;
+  }
+};
+
+// bbm::orennayar (include/bsdfmodel/orennayar.h:22-137); params: albedo RGB, roughness.  A and B
+// are double expressions of the roughness (rounded to float once per thread); sample and pdf are
+// Lambertian's.
+struct OrenNayar
+{
+  static constexpr int kParams = 4;
+  static constexpr uint32_t kComponent = kFlagDiffuse;
+  float alb_pi[3], A, B;
+  __device__ explicit OrenNayar(const float* p)
+  {
+    const float sigma2 = p[3] * p[3];
+    A = float(1 - 0.5 * sigma2 / (sigma2 + 0.33));
+    B = float(0.45 * sigma2 / (sigma2 + 0.09));
+    // albedo / Constants::Pi(): once per thread, IEEE division
+    alb_pi[0] = p[0] / kPiF; alb_pi[1] = p[1] / kPiF; alb_pi[2] = p[2] / kPiF;
+  }
+
+  // orennayar.h:50-72 eval: strict z > 0; factor = A + B max(dot_xy, 0) / max(z_in, z_out)
+  template<int MODE>
+  __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
+  {
+    const bool diff = component & kFlagDiffuse;
+    const bool m = diff && (in.z > 0) && (out.z > 0);
+    const float cos_beta = fmaxf(in.z, out.z);
+    const float dot_xy = (in.x * out.x) + (in.y * out.y);
+    const float factor = A + div_nr(B * fmaxf(dot_xy, 0.0f), cos_beta);
+    rgb[0] = m ? alb_pi[0] * factor : 0.0f;
+    rgb[1] = m ? alb_pi[1] * factor : 0.0f;
+    rgb[2] = m ? alb_pi[2] * factor : 0.0f;
+    pdf = (diff && (in.z >= 0) && (out.z >= 0)) ? in.z * kInvPiF : 0.0f;
+  }
+
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    const float unit_albedo[3] = {1.0f, 1.0f, 1.0f};
+    Lambertian(unit_albedo).sample(out, xi0, xi1, component, dir, pdf, flag);
   }
 };
 

@@ -1,0 +1,437 @@
+// bbm_amd/csrc/kernels.hpp -- the streaming kernels and their host-side launchers, templated on
+// the model composition.  Included by the per-family instantiation units (inst_*.hip), which
+// explicitly instantiate launch_eval_pdf<M> / launch_sample<M> for their models, and by the
+// registry unit (bbm_hip.hip), which only takes their addresses (extern template).
+//
+// Layout and launch: directions are SoA float32 in HBM; one thread owns four
+// consecutive pairs, so each lane issues one 16-byte load per input array and one 16-byte store
+// per output array -- every wave instruction moves a full 1 KiB, coalesced.  The grid covers the
+// batch (one 256-thread workgroup per 1024 pairs); work is per-pair independent, so no LDS, no
+// atomics and no inter-workgroup traffic are needed.  Parameters are passed by value in the
+// kernarg segment and stay in SGPRs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <string>
+
+#include "../../include/bbm_hip.h"
+#include "math.hpp"
+#include "microfacet.hpp"
+
+namespace bbmhip {
+
+constexpr int kMaxParams = 64;
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = 1 << 22;   // effectively one workgroup per 1024 pairs (full grid)
+
+// Record `msg` as the calling thread's last error (bbm_hip_last_error) and return `code`.
+int fail(int code, const std::string& msg);
+
+struct ParamBlock { float v[kMaxParams]; };
+
+struct EvalArgs
+{
+  const float* ix; const float* iy; const float* iz;
+  const float* ox; const float* oy; const float* oz;
+  const uint8_t* mask;
+  float* r; float* g; float* b; float* pdf;
+  uint64_t n;
+  uint32_t component;
+  ParamBlock p;
+};
+
+template<class Model, int MODE>
+__device__ __forceinline__ void one_pair(const Model& m, const EvalArgs& a, uint64_t i, bool active)
+{
+  float rgb[3], pdf;
+  const v3 in = mk3(a.ix[i], a.iy[i], a.iz[i]);
+  const v3 out = mk3(a.ox[i], a.oy[i], a.oz[i]);
+  m.template eval_pdf<MODE>(in, out, active ? a.component : 0u, rgb, pdf);
+  if (MODE & kModeEval) { a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2]; }
+  if (MODE & kModePdf) a.pdf[i] = pdf;
+}
+
+// Vector path: 4 consecutive pairs per thread-iteration, 16-byte loads/stores per array.
+// Requires every array 16-byte aligned (checked on the host); the n % 4 tail runs scalar.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template<bool NT>
+__device__ __forceinline__ float4 ld4(const float* p, uint64_t t)
+{
+  if (NT)
+  {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p) + t);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return reinterpret_cast<const float4*>(p)[t];
+}
+
+template<bool NT>
+__device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, float c, float d)
+{
+  if (NT) __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
+  else reinterpret_cast<float4*>(p)[t] = make_float4(a, b, c, d);
+}
+
+#ifndef BBM_HIP_SGPR_LIMIT
+#define BBM_HIP_KERNEL_ATTR
+#else
+// Cap the SGPR budget: 256-thread workgroups are admitted per CU only up to
+// floor(800 / (ceil(sgpr/16)*16 + 16)) (MI355X_MICROARCH.md, Residency) -- 98 SGPRs = 6 per CU.
+#define BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_num_sgpr(BBM_HIP_SGPR_LIMIT)))
+#endif
+
+template<class Model, int MODE, bool MASK, bool NT>
+__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v4(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
+  {
+    const float4 ix = ld4<NT>(a.ix, t);
+    const float4 iy = ld4<NT>(a.iy, t);
+    const float4 iz = ld4<NT>(a.iz, t);
+    const float4 ox = ld4<NT>(a.ox, t);
+    const float4 oy = ld4<NT>(a.oy, t);
+    const float4 oz = ld4<NT>(a.oz, t);
+    uint32_t mk = 0x01010101u;
+    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
+    const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
+    float r[4], g[4], b[4], p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      float rgb[3];
+      const uint32_t comp = ((mk >> (8 * j)) & 0xffu) ? a.component : 0u;
+      m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
+      r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
+    }
+    if (MODE & kModeEval)
+    {
+      st4<NT>(a.r, t, r[0], r[1], r[2], r[3]);
+      st4<NT>(a.g, t, g[0], g[1], g[2], g[3]);
+      st4<NT>(a.b, t, b[0], b[1], b[2], b[3]);
+    }
+    if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+// Eight pairs per thread: two quads, each a fully coalesced 1 KiB wave access (quad t and quad
+// t + 64 within the wave's 128-quad tile).  More independent work per wave for the scheduler.
+template<class Model, int MODE, bool MASK, bool NT>
+__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v8(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t stride = uint64_t(gridDim.x) * (2 * kBlock);
+  for (uint64_t base = uint64_t(blockIdx.x) * (2 * kBlock) + wave * 128; base < n4; base += stride)
+  {
+    uint64_t tq[2] = {base + lane, base + 64 + lane};
+    float4 c[2][6];
+    uint32_t cm[2] = {0x01010101u, 0x01010101u};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      const uint64_t t = tq[u] < n4 ? tq[u] : n4 - 1;
+      c[u][0] = ld4<NT>(a.ix, t); c[u][1] = ld4<NT>(a.iy, t); c[u][2] = ld4<NT>(a.iz, t);
+      c[u][3] = ld4<NT>(a.ox, t); c[u][4] = ld4<NT>(a.oy, t); c[u][5] = ld4<NT>(a.oz, t);
+      if (MASK) cm[u] = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    }
+    float r[2][4], g[2][4], b[2][4], p[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      const float inx[4] = {c[u][0].x, c[u][0].y, c[u][0].z, c[u][0].w}, iny[4] = {c[u][1].x, c[u][1].y, c[u][1].z, c[u][1].w};
+      const float inz[4] = {c[u][2].x, c[u][2].y, c[u][2].z, c[u][2].w}, onx[4] = {c[u][3].x, c[u][3].y, c[u][3].z, c[u][3].w};
+      const float ony[4] = {c[u][4].x, c[u][4].y, c[u][4].z, c[u][4].w}, onz[4] = {c[u][5].x, c[u][5].y, c[u][5].z, c[u][5].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        float rgb[3];
+        const uint32_t comp = ((cm[u] >> (8 * j)) & 0xffu) ? a.component : 0u;
+        m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[u][j]);
+        r[u][j] = rgb[0]; g[u][j] = rgb[1]; b[u][j] = rgb[2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+    {
+      if (tq[u] >= n4) continue;
+      const uint64_t t = tq[u];
+      if (MODE & kModeEval)
+      {
+        st4<NT>(a.r, t, r[u][0], r[u][1], r[u][2], r[u][3]);
+        st4<NT>(a.g, t, g[u][0], g[u][1], g[u][2], g[u][3]);
+        st4<NT>(a.b, t, b[u][0], b[u][1], b[u][2], b[u][3]);
+      }
+      if (MODE & kModePdf) st4<NT>(a.pdf, t, p[u][0], p[u][1], p[u][2], p[u][3]);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+// Software-pipelined grid-stride variant: the six 16-byte loads of the thread's NEXT quad are
+// issued before the current quad is computed, so every wave keeps HBM reads in flight while its
+// VALU work runs (the plain kernel only overlaps load and compute across different waves).
+template<class Model, int MODE, bool MASK, bool NT>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_pipe(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t < n4)
+  {
+    float4 c[6];
+    uint32_t cm = 0x01010101u;
+    c[0] = ld4<NT>(a.ix, t); c[1] = ld4<NT>(a.iy, t); c[2] = ld4<NT>(a.iz, t);
+    c[3] = ld4<NT>(a.ox, t); c[4] = ld4<NT>(a.oy, t); c[5] = ld4<NT>(a.oz, t);
+    if (MASK) cm = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    for (; t < n4; t += stride)
+    {
+      const uint64_t tn = (t + stride < n4) ? t + stride : t;   // clamped: the last prefetch re-reads
+      float4 nx[6];
+      uint32_t nm = 0x01010101u;
+      nx[0] = ld4<NT>(a.ix, tn); nx[1] = ld4<NT>(a.iy, tn); nx[2] = ld4<NT>(a.iz, tn);
+      nx[3] = ld4<NT>(a.ox, tn); nx[4] = ld4<NT>(a.oy, tn); nx[5] = ld4<NT>(a.oz, tn);
+      if (MASK) nm = reinterpret_cast<const uint32_t*>(a.mask)[tn];
+      const float inx[4] = {c[0].x, c[0].y, c[0].z, c[0].w}, iny[4] = {c[1].x, c[1].y, c[1].z, c[1].w};
+      const float inz[4] = {c[2].x, c[2].y, c[2].z, c[2].w}, onx[4] = {c[3].x, c[3].y, c[3].z, c[3].w};
+      const float ony[4] = {c[4].x, c[4].y, c[4].z, c[4].w}, onz[4] = {c[5].x, c[5].y, c[5].z, c[5].w};
+      float r[4], g[4], b[4], p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        float rgb[3];
+        const uint32_t comp = ((cm >> (8 * j)) & 0xffu) ? a.component : 0u;
+        m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
+        r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
+      }
+      if (MODE & kModeEval)
+      {
+        st4<NT>(a.r, t, r[0], r[1], r[2], r[3]);
+        st4<NT>(a.g, t, g[0], g[1], g[2], g[3]);
+        st4<NT>(a.b, t, b[0], b[1], b[2], b[3]);
+      }
+      if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) c[k] = nx[k];
+      cm = nm;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+// Scalar path for unaligned arrays.
+template<class Model, int MODE, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+}
+
+// Grid cap for the grid-stride kernels; BBM_HIP_MAX_BLOCKS overrides it (tuning experiments).
+inline uint64_t max_blocks()
+{
+  static const uint64_t v = [] {
+    const char* e = std::getenv("BBM_HIP_MAX_BLOCKS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? uint64_t(x) : uint64_t(kMaxBlocks);
+  }();
+  return v;
+}
+
+// Pairs per thread of the vector kernel (BBM_HIP_PPT=8 selects k_eval_pdf_v8; tuning experiments).
+inline int pairs_per_thread()
+{
+  static const int v = [] {
+    const char* e = std::getenv("BBM_HIP_PPT");
+    return (e && std::atoi(e) == 8) ? 8 : 4;
+  }();
+  return v;
+}
+
+// Software-pipelined grid-stride kernel (BBM_HIP_PIPE=1; tuning experiments).
+inline bool use_pipe()
+{
+  static const bool v = [] {
+    const char* e = std::getenv("BBM_HIP_PIPE");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
+// Streaming stores/loads with the nontemporal hint (BBM_HIP_NT=0 disables; tuning experiments).
+inline bool use_nt()
+{
+  static const bool v = [] {
+    const char* e = std::getenv("BBM_HIP_NT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// ------------------------------------------------------------------------------- sample
+
+struct SampleArgs
+{
+  const float* ox; const float* oy; const float* oz;
+  const float* xi0; const float* xi1;
+  const uint8_t* mask;
+  float* dx; float* dy; float* dz; float* pdf; uint32_t* flag;
+  uint64_t n;
+  uint32_t component;
+  ParamBlock p;
+};
+
+template<class Model>
+__device__ __forceinline__ void one_sample(const Model& m, const SampleArgs& a, uint64_t i, bool active)
+{
+  v3 d; float pdf; uint32_t f;
+  m.sample(mk3(a.ox[i], a.oy[i], a.oz[i]), a.xi0[i], a.xi1[i], active ? a.component : 0u, d, pdf, f);
+  a.dx[i] = d.x; a.dy[i] = d.y; a.dz[i] = d.z; a.pdf[i] = pdf; a.flag[i] = f;
+}
+
+// 4 samples per thread-iteration: 5 x 16-byte loads (out xyz, xi0, xi1), 5 x 16-byte stores.
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_sample_v4(SampleArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
+  {
+    const float4 ox = reinterpret_cast<const float4*>(a.ox)[t];
+    const float4 oy = reinterpret_cast<const float4*>(a.oy)[t];
+    const float4 oz = reinterpret_cast<const float4*>(a.oz)[t];
+    const float4 x0 = reinterpret_cast<const float4*>(a.xi0)[t];
+    const float4 x1 = reinterpret_cast<const float4*>(a.xi1)[t];
+    uint32_t mk = 0x01010101u;
+    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
+    const float u0[4] = {x0.x, x0.y, x0.z, x0.w}, u1[4] = {x1.x, x1.y, x1.z, x1.w};
+    float dx[4], dy[4], dz[4], pd[4];
+    uint32_t fl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      v3 d;
+      const uint32_t comp = ((mk >> (8 * j)) & 0xffu) ? a.component : 0u;
+      m.sample(mk3(onx[j], ony[j], onz[j]), u0[j], u1[j], comp, d, pd[j], fl[j]);
+      dx[j] = d.x; dy[j] = d.y; dz[j] = d.z;
+    }
+    reinterpret_cast<float4*>(a.dx)[t] = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    reinterpret_cast<float4*>(a.dy)[t] = make_float4(dy[0], dy[1], dy[2], dy[3]);
+    reinterpret_cast<float4*>(a.dz)[t] = make_float4(dz[0], dz[1], dz[2], dz[3]);
+    reinterpret_cast<float4*>(a.pdf)[t] = make_float4(pd[0], pd[1], pd[2], pd[3]);
+    reinterpret_cast<uint4*>(a.flag)[t] = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_sample<Model>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_sample_v1(SampleArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    one_sample<Model>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template<class Model, int MODE, bool MASK>
+int launch_mode(const EvalArgs& a, hipStream_t s)
+{
+  bool vec = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
+             aligned16(a.oz) && (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
+  if (MODE & kModeEval) vec = vec && aligned16(a.r) && aligned16(a.g) && aligned16(a.b);
+  if (MODE & kModePdf) vec = vec && aligned16(a.pdf);
+  const uint64_t units = vec ? (a.n >> 2) : a.n;
+#ifdef BBM_HIP_EXPERIMENTAL
+  // A/B variants (tools/gpu_ab.sh): 8 pairs/thread, software pipelining, temporal loads/stores.
+  const uint64_t per_block = (vec && pairs_per_thread() == 8) ? 2 * kBlock : kBlock;
+#else
+  const uint64_t per_block = kBlock;
+#endif
+  uint64_t blocks = (units + per_block - 1) / per_block;
+  if (blocks < 1) blocks = 1;
+  if (blocks > max_blocks()) blocks = max_blocks();
+#ifdef BBM_HIP_EXPERIMENTAL
+  if (vec && pairs_per_thread() == 8)
+    hipLaunchKernelGGL((k_eval_pdf_v8<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec && use_pipe()) hipLaunchKernelGGL((k_eval_pdf_pipe<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec && !use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, false>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else
+#endif
+  if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+template<class Model, bool MASK>
+int launch_sample_mask(const SampleArgs& a, hipStream_t s)
+{
+  const bool vec = aligned16(a.ox) && aligned16(a.oy) && aligned16(a.oz) && aligned16(a.xi0) && aligned16(a.xi1) &&
+                   aligned16(a.dx) && aligned16(a.dy) && aligned16(a.dz) && aligned16(a.pdf) && aligned16(a.flag) &&
+                   (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
+  const uint64_t units = vec ? (a.n >> 2) : a.n;
+  uint64_t blocks = (units + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > max_blocks()) blocks = max_blocks();
+  if (vec) hipLaunchKernelGGL((k_sample_v4<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_sample_v1<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+template<class Model>
+int launch_sample(const SampleArgs& a, hipStream_t s)
+{
+  return a.mask ? launch_sample_mask<Model, true>(a, s) : launch_sample_mask<Model, false>(a, s);
+}
+
+template<class Model>
+int launch_eval_pdf(const EvalArgs& a, int mode, hipStream_t s)
+{
+  const bool mk = a.mask != nullptr;
+  switch (mode)
+  {
+    case kModeEval: return mk ? launch_mode<Model, kModeEval, true>(a, s) : launch_mode<Model, kModeEval, false>(a, s);
+    case kModePdf: return mk ? launch_mode<Model, kModePdf, true>(a, s) : launch_mode<Model, kModePdf, false>(a, s);
+    default: return mk ? launch_mode<Model, kModeEvalPdf, true>(a, s) : launch_mode<Model, kModeEvalPdf, false>(a, s);
+  }
+}
+
+using EvalLauncher = int (*)(const EvalArgs&, int, hipStream_t);
+using SampleLauncher = int (*)(const SampleArgs&, hipStream_t);
+
+}  // namespace bbmhip

@@ -25,6 +25,10 @@ constexpr double kInvSqrtPiD = 0.564189583547756286948079451560772586;
 constexpr float kPiF = float(1.0f * kPiD);
 constexpr float kInvPiF = float(1.0f * kInvPiD);
 constexpr float kInvSqrtPiF = float(1.0f * kInvSqrtPiD);
+constexpr float kPi2F = float(2.0f * kPiD);          // Constants::Pi(2)
+constexpr float kPi4F = float(4.0f * kPiD);          // Constants::Pi(4)
+constexpr float kPi8F = float(8.0f * kPiD);          // Constants::Pi(8)
+constexpr float kInvPiHalfF = float(0.5f * kInvPiD); // Constants::InvPi(0.5)
 constexpr float kEpsF = 1.1920928955078125e-07f;   // numeric_limits<float>::epsilon()
 
 struct v3 { float x, y, z; };

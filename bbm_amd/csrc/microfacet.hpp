@@ -308,6 +308,54 @@ struct HeightCorrelated
   }
 };
 
+// ndf::low (include/ndf/low.h:32-141): the unnormalised ABC "S" term of [Low 2012] as an NDF.
+// eval pow(1 + B (1 - z), -C) in double; pdf = eval B (1/(2 pi)) normalization with the
+// normalization a per-thread double constant; sample inverts the marginal CDF of cos(theta)
+// (not a visible-normal sampler: the view is ignored); G1 = 1 (Low uses v-groove shadowing).
+struct LowNdf
+{
+  static constexpr int kParams = 2;
+  float B, C, norm_pdf;
+  double lg1pB, pw1pB, inv_exp;
+  bool c_is_one;
+  __device__ explicit LowNdf(const float* p) : B(p[0]), C(p[1])
+  {
+    c_is_one = fabsf(C - 1) < kEpsF;
+    lg1pB = log(1.0 + B);
+    pw1pB = pow(1.0 + B, 1.0 - C);
+    inv_exp = -1.0 / (C - 1.0);
+    const float normalization = float(c_is_one ? 1.0f / lg1pB : (C - 1.0) / (1.0 - pw1pB));
+    norm_pdf = kInvPiHalfF * normalization;
+  }
+
+  __device__ __forceinline__ float eval(v3 h) const
+  {
+    const float S = float(pow(1.0 + B * (1.0 - h.z), double(-C)));
+    return (h.z > 0) ? S : 0.0f;
+  }
+
+  __device__ __forceinline__ float G1(v3, v3) const { return 1.0f; }
+
+  // low.h:67-89
+  __device__ __forceinline__ v3 sample(v3, float xi0, float xi1) const
+  {
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
+    const float term = float(c_is_one ? exp(xi0 * lg1pB) : pow(1.0 + xi0 * (pw1pB - 1.0), inv_exp));
+    const float cosT = float((1.0 + B - term) / B);
+    const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
+    float sp, cp;
+    sincosf(xi1 * float(2.0f * kPiD), &sp, &cp);
+    return mk3(cp * sinT, sp * sinT, cosT);
+  }
+
+  // low.h:96-112: mask m.z > 0 (via eval) and pdf > 0
+  __device__ __forceinline__ float pdf(v3, v3, float D) const
+  {
+    const float p = D * B * norm_pdf;
+    return (p > 0) ? p : 0.0f;
+  }
+};
+
 // ---------------------------------------------------------------------------- fresnel
 
 // fresnel::cook with a scalar ior (include/bbm/fresnel_cook.h:41-56)

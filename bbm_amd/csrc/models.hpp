@@ -1,0 +1,52 @@
+// bbm_amd/csrc/models.hpp -- the model compositions the library implements (one line per
+// reference model, file:line of its definition), and the X-macro lists the instantiation units
+// and the registry iterate over.
+#pragma once
+#include "diffuse.hpp"
+#include "lobes.hpp"
+#include "microfacet.hpp"
+
+namespace bbmhip {
+
+// Compositions (reference file:line):
+using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;         // bsdfmodel/cooktorrance.h:28-34
+using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                        // bsdfmodel/ggx.h:27-33
+using CookTorranceWalterM = Microfacet<Beckmann<false, true>, Uncorrelated, FresnelCook, Norm::Walter, true>;  // bsdfmodel/cooktorrancewalter.h:32-38
+
+using CookTorranceHeitzM = Microfacet<Beckmann<true, true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;   // bsdfmodel/cooktorranceheitz.h:33-39
+using GGXHeitzM = Microfacet<GGX<true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;                     // bsdfmodel/ggxheitz.h:28-34
+using NganCookTorranceM = Microfacet<Beckmann<false, true>, VGroove, FresnelSchlick, Norm::Cook, true>;         // bsdfmodel/ngan.h:141-147
+using PhongWalterM = Microfacet<PhongNdf, Uncorrelated, FresnelCook, Norm::Walter, true>;                         // bsdfmodel/phongwalter.h:27-33
+using RibardiereM = Microfacet<StudentT<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                   // bsdfmodel/ribardiere.h:28-34
+using RibardiereAnisoM = Microfacet<StudentT<true>, Uncorrelated, FresnelCook, Norm::Walter, true>;              // bsdfmodel/ribardiere.h:46-52
+
+using LowMicrofacetM = Microfacet<LowNdf, VGroove, FresnelCook, Norm::Cook, true>;                             // bsdfmodel/lowmicrofacet.h:37-70, low.h:40-41
+using WardM = Ward<0, true>;                  // bsdfmodel/ward.h:26-168
+using WardDuerM = Ward<1, true>;              // bsdfmodel/wardduer.h:29-81
+using WardDGMM = Ward<2, true>;               // bsdfmodel/wardduergeislermoroder.h:29-81
+using NganWardM = Ward<0, false>;             // bsdfmodel/ngan.h:30-31
+using NganWardDuerM = Ward<1, false>;         // bsdfmodel/ngan.h:37-38
+using LafortuneM = Lafortune<true, false>;    // bsdfmodel/lafortune.h:28-172
+using NganLafortuneM = Lafortune<false, true>;   // bsdfmodel/ngan.h:54-129
+using ASM = AshikhminShirley<FresnelSchlickRGB, true, false, false>;                       // ashikhminshirley.h:29-221
+using ASFullM = AshikhminShirley<FresnelSchlickRGB, true, false, true>;                    // ashikhminshirleyfull.h:31-191
+using LowASM = AshikhminShirley<ScalarFresnel3<FresnelCook>, false, true, false>;          // bsdfmodel/low.h:24-25
+using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, false>;      // bsdfmodel/ngan.h:157-158
+
+}  // namespace bbmhip
+
+// X(composition) per instantiation unit
+#define BBM_HIP_MICROFACET_MODELS(X) \
+  X(CookTorranceM) X(GGXM) X(CookTorranceWalterM) X(CookTorranceHeitzM) X(GGXHeitzM) X(NganCookTorranceM) \
+  X(PhongWalterM) X(RibardiereM) X(RibardiereAnisoM) X(LowMicrofacetM)
+#define BBM_HIP_LOBE_MODELS(X) \
+  X(WardM) X(WardDuerM) X(WardDGMM) X(NganWardM) X(NganWardDuerM) X(PhongLobe) X(LafortuneM) X(NganLafortuneM) \
+  X(ASM) X(ASFullM) X(LowASM) X(NganASM) X(LowSmooth)
+#define BBM_HIP_DIFFUSE_MODELS(X) X(Lambertian) X(OrenNayar)
+
+#define BBM_HIP_INSTANTIATE(M)                                                   \
+  template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);           \
+  template int launch_sample<M>(const SampleArgs&, hipStream_t);
+#define BBM_HIP_EXTERN(M)                                                        \
+  extern template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);    \
+  extern template int launch_sample<M>(const SampleArgs&, hipStream_t);
