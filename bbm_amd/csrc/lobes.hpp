@@ -456,9 +456,9 @@ struct LowSmooth
     const float ro2 = sin_theta2(out);
     const float bb = B * (1 - ro2);
     float temp = float(1.0 + (2 * B * (1.0 + ro2)) + double(bb * bb));
-    temp = float(-log(2.0) + double(logf(1 + B * (1 - ro2) + safe_sqrtf(temp))));
+    temp = float(-log(2.0) + double(logf_cr(1 + B * (1 - ro2) + safe_sqrtf(temp))));
     const float mdpi = B * div_nr(1.0f, temp);
-    const float E = float(2.0 * double(expf(xi0 * B * div_nr(1.0f, mdpi))));
+    const float E = float(2.0 * double(expf_cr(xi0 * B * div_nr(1.0f, mdpi))));
     const float ri = safe_sqrtf(div_nr((E - 2) * (E + 2 * B * ro2), 2 * E * B));
     const float ro = sqrtf(ro2);
     const double rp = double(ri + ro), rm = double(ri - ro);

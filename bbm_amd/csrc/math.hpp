@@ -179,4 +179,11 @@ __device__ __forceinline__ double erfinv_d(float a)
 // correctly rounded square is what glibc's powf returns.
 __device__ __forceinline__ float pow2f(float x) { return x * x; }
 
+// expf rounded from the f64 exponential: the float nearest e^x except within ~2^-29 ulp of a
+// midpoint, i.e. what the reference's (glibc, ~0.5 ulp) expf returns.  Used where the result is
+// cancelled against a constant right after (Low smooth sampling's E - 2 as xi0 -> 0), so that a
+// 1-ulp expf difference is not amplified; the eval kernels keep the full-rate f32 expf.
+__device__ __forceinline__ float expf_cr(float x) { return float(exp(double(x))); }
+__device__ __forceinline__ float logf_cr(float x) { return float(log(double(x))); }
+
 }  // namespace bbmhip
