@@ -42,8 +42,11 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="after the W warmup steps, keep stepping (untimed) until this much wall time has passed "
+                         "since warmup began: MI355X clocks take ~50 back-to-back launches to settle after a load change")
     ap.add_argument("--pairs", type=int, default=100_000_000, help="pairs per GPU")
     ap.add_argument("--model", default="CookTorrance")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -113,9 +116,16 @@ def main():
     pdf = torch.empty((n,), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream()
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         model.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=stream)
     torch.cuda.synchronize()
+    settle_steps = 0
+    while time.perf_counter() - tw < args.settle_s:
+        for _ in range(10):
+            model.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=stream)
+        settle_steps += 10
+        torch.cuda.synchronize()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -175,6 +185,7 @@ def main():
                          "kernel": f"k_eval_pdf_v4<{args.model}>", "kernel_ms": kern_ms,
                          "bytes_per_pair": bpp},
             "outputs_ok": ok,
+            "settle": {"seconds": args.settle_s, "extra_untimed_steps": settle_steps},
         }
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(model, din, dout, args.cpu_seconds)
