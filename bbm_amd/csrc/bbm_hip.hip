@@ -25,6 +25,7 @@ int fail(int code, const std::string& msg)
 BBM_HIP_MICROFACET_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_LOBE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_DIFFUSE_MODELS(BBM_HIP_EXTERN)
+BBM_HIP_SPECTRAL_MODELS(BBM_HIP_EXTERN)
 
 namespace {
 
@@ -106,6 +107,14 @@ const ModelEntry kModels[] = {
    {0.5f, 0.5f, 0.5f, 0.1f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, 1, kFMax}},
   {"LowSmooth", 6, kFlagSpecular, &launch_eval_pdf<LowSmooth>, &launch_sample<LowSmooth>,
    {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}},
+  // bsdfmodel/bagher.h:62-68: albedo, K, Lambda, c, theta0, k (ndf/sgd.h:197-203, Dependent),
+  // alpha, p (sgd.h:107-111), eta = (F0, F1) RGB (bagher.h:31, default {1, 0}, lower {0, -1})
+  {"Bagher", 30, kFlagSpecular, &launch_eval_pdf<Bagher>, &launch_sample<Bagher>,
+   {0.5f, 0.5f, 0.5f, 7.5f, 7.5f, 7.5f, 1, 1, 1, 1, 1, 1, 1.5707963705062866f, 1.5707963705062866f, 1.5707963705062866f,
+    1, 1, 1, 0.1f, 0.1f, 0.1f, 0.64f, 0.64f, 0.64f, 1, 1, 1, 0, 0, 0},
+   {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, kEpsF, kEpsF, kEpsF, 0, 0, 0, 0, 0, 0, -1, -1, -1},
+   {1, 1, 1, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax,
+    1, 1, 1, kFMax, kFMax, kFMax, 1, 1, 1, 1, 1, 1}},
 };
 constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
@@ -114,7 +123,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && WardM::kParams == 5 && NganWardM::kParams == 4 &&
               PhongLobe::kParams == 4 && LafortuneM::kParams == 7 && NganLafortuneM::kParams == 6 &&
               ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 && NganASM::kParams == 5 &&
-              LowSmooth::kParams == 6, "registry nparams must match the compositions");
+              LowSmooth::kParams == 6 && Bagher::kParams == 30, "registry nparams must match the compositions");
 
 const ModelEntry* entry(int id) { return (id >= 0 && id < kNumModels) ? &kModels[id] : nullptr; }
 

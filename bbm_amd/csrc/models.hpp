@@ -5,6 +5,7 @@
 #include "diffuse.hpp"
 #include "lobes.hpp"
 #include "microfacet.hpp"
+#include "spectral.hpp"
 
 namespace bbmhip {
 
@@ -43,6 +44,7 @@ using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, fa
   X(WardM) X(WardDuerM) X(WardDGMM) X(NganWardM) X(NganWardDuerM) X(PhongLobe) X(LafortuneM) X(NganLafortuneM) \
   X(ASM) X(ASFullM) X(LowASM) X(NganASM) X(LowSmooth)
 #define BBM_HIP_DIFFUSE_MODELS(X) X(Lambertian) X(OrenNayar)
+#define BBM_HIP_SPECTRAL_MODELS(X) X(Bagher)
 
 #define BBM_HIP_INSTANTIATE(M)                                                   \
   template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);           \

@@ -1,0 +1,120 @@
+// bbm_amd/csrc/spectral.hpp -- microfacet models whose NDF, shadowing and Fresnel terms are
+// Spectrum-valued (one value per RGB channel), i.e. Bagher et al.'s Shifted Gamma Distribution
+// model (include/bsdfmodel/bagher.h:62-68):
+//
+//   scaledmodel< microfacet< ndf::sgd, maskingshadowing::uncorrelated, fresnel::bagher, Cook (pi) > >
+//
+// Parameters (attribute declaration order, bbm::parameter_values incl. Dependent, 30 floats):
+//   albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3]   (ndf::sgd, ndf/sgd.h:197-203)
+//   alpha[3], p[3]                                     (ndf::sgd_base, ndf/sgd.h:107-111)
+//   eta[2][3] = (F0 RGB, F1 RGB)                       (fresnel::bagher, bagher.h:27-57)
+// Sampling and pdf use a GGX<Isotropic> lobe with the channel-averaged alpha (ndf/sgd.h:73-93).
+//
+// The per-pair geometry (halfway vector, its tan^2, theta(in), theta(out), cos(theta_h)^4) is
+// channel-independent and computed once; only the channel terms run three times.
+#pragma once
+#include "microfacet.hpp"
+
+namespace bbmhip {
+
+// spherical::theta(v) for z(v) >= 0 (include/core/spherical.h:26-32):
+// 2.0 * asin(0.5 * |v - (0,0,sign(z))|) in double, returned as float; for z < 0, Pi - that.
+__device__ __forceinline__ float theta_of(v3 v)
+{
+  const float sz = (v.z < 0.0f) ? -1.0f : 1.0f;          // bbm::sign = copysign(1, z)
+  const float dz = v.z - sz;
+  const float nrm = sqrtf(((0.0f + v.x * v.x) + v.y * v.y) + dz * dz);
+  const double t = 2.0 * asin(0.5 * double(nrm));
+  return (v.z >= 0) ? float(t) : float(double(kPiF) - t);
+}
+
+struct Bagher
+{
+  static constexpr int kParams = 30;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  float albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3];
+  GGX<false> ggx;   // sampling / pdf lobe (ndf/sgd.h:73-93)
+
+  __device__ static float avg_alpha(const float* a) { return div_nr(((0.0f + a[0]) + a[1]) + a[2], 3.0f); }
+
+  __device__ explicit Bagher(const float* q) : ggx(q + 18)
+  {
+    for (int j = 0; j < 3; ++j)
+    {
+      albedo[j] = q[j]; K[j] = q[3 + j]; Lambda[j] = q[6 + j]; c[j] = q[9 + j]; theta0[j] = q[12 + j];
+      k[j] = q[15 + j]; alpha[j] = q[18 + j]; p[j] = q[21 + j]; F0[j] = q[24 + j]; F1[j] = q[27 + j];
+    }
+    ggx.au = ggx.av = avg_alpha(alpha);
+  }
+
+  // ndf::sgd::G1 per channel (ndf/sgd.h:157-193), for a direction with theta(v) = th
+  __device__ __forceinline__ float G1(int j, float th) const
+  {
+    const float g = 1.0f + Lambda[j] * (1.0f - expf(c[j] * powf(th - theta0[j], k[j])));
+    return (th > theta0[j]) ? g : 1.0f;
+  }
+
+  template<int MODE>
+  __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z > 0.0f) && (out.z > 0.0f);
+    const v3 h = halfway(in, out);
+    const float outh = dot3(out, h);
+    if (MODE & kModeEval)
+    {
+      const float inh = dot3(in, h);
+      const float tan2 = tan_theta2(h);
+      const double z2 = double(h.z) * double(h.z);
+      const double dnorm = double(kPiF) * (z2 * z2);      // Constants::Pi() * pow(cos, 4.0) (sgd.h:62)
+      // uncorrelated (uncorrelated.h:30-42) + sgd::G1 masks: z(v) > 0 and v.m > 0 for both
+      const bool gmask = (inh > 0) && (outh > 0);
+      const float th_in = theta_of(in), th_out = theta_of(out);
+      const float cosF = 0.5f * (inh + outh);
+      const double x = double(1.0f - cosF);
+      const double x5 = (x * x) * (x * x) * x;
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+      {
+        // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
+        const float t = alpha[j] + div_nr(tan2, alpha[j]);
+        const float den = powf(t, p[j]);
+        const float P22 = (den > kEpsF) ? div_nr(expf(-t), den) : 0.0f;
+        const float Dj = ((h.z > 0) ? f_div_d(double(P22), dnorm) : 0.0f) * K[j];
+        const float Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0f;
+        // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
+        const float S = float(double(F0[j]) + double(1.0f - F0[j]) * x5);
+        const float Fj = S - F1[j] * cosF;
+        const float res = eval_scale<Norm::Cook>((Dj * Gj) * Fj, in.z * out.z);
+        rgb[j] = active ? res * albedo[j] : 0.0f;
+      }
+    }
+    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    if (MODE & kModePdf)
+    {
+      const float Dg = ggx.eval(h);
+      const float pp = div_nr(ggx.pdf(out, h, Dg), 4.0f * fabsf(outh));
+      pdf = active ? pp : 0.0f;
+    }
+    else pdf = 0.0f;
+  }
+
+  // microfacet.h:115-141 with the GGX(avg alpha) visible-normal sampler
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f);
+    pdf = 0.0f;
+    flag = kFlagNone;
+    if (!(component & kFlagSpecular)) return;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+    if (!(out.z > 0)) return;
+    const v3 m = ggx.sample(out, xi0, xi1);
+    const float d = dot3(m, out);
+    dir = mk3(2.0f * (m.x * d) - out.x, 2.0f * (m.y * d) - out.y, 2.0f * (m.z * d) - out.z);
+    float rgb[3];
+    eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+
+}  // namespace bbmhip
