@@ -9,16 +9,17 @@ name, `fromString` / `bsdf_import`, `bsdf_flag`, `unit_t`, `BsdfSample`, and bat
 Importing the package loads the HIP library; if it is missing the import fails loudly.
 """
 from . import _lib
-from .backbone import (BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString, model_names,
-                       unit_t, _make_ctor)
+from .backbone import (Aggregate, BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString,
+                       model_names, unit_t, _make_ctor)
 from .models import ATTRIBUTES
 
 _lib.load()
 
-__all__ = ["BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
+__all__ = ["Aggregate", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
            "fill_directions", "ATTRIBUTES"]
 
 for _name in model_names():
-    globals()[_name] = _make_ctor(_name)
-    __all__.append(_name)
+    if _name.isidentifier():          # Aggregate<Lambertian,X> entries are built with Aggregate(...)
+        globals()[_name] = _make_ctor(_name)
+        __all__.append(_name)
 del _name

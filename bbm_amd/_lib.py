@@ -38,7 +38,13 @@ SIGNATURES = {
     "bbm_hip_pdf": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P]),
     "bbm_hip_eval_pdf": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
     "bbm_hip_sample": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "bbm_hip_reflectance": (_I, [_I, _P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
     "bbm_hip_fill_directions": (_I, [_U64, _U32, _U64, _SZ, _I, _P, _P, _P, _P]),
+    "bbm_hip_model_param_attrs": (_I, [_I, _P, _I]),
+    "bbm_hip_linearizer_size": (_I, [_P, _P]),
+    "bbm_hip_linearize": (_I, [_P, _U64, _SZ, _P, _P, _P, _P, _P, _P, _P]),
+    "bbm_hip_loss_workspace_size": (_SZ, [_I]),
+    "bbm_hip_loss": (_I, [_I, _P, _I, _I, _P, _U64, _SZ, _P, _P, _P, _I, _U32, _U32, _P, _P, _SZ, _P]),
 }
 
 

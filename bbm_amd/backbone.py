@@ -20,7 +20,7 @@ import re
 import numpy as np
 
 from . import _lib
-from .models import ATTRIBUTES, attr_size, nparams, to_string
+from .models import AGGREGATES, ATTRIBUTES, aggregate_key, attr_size, nparams, to_string
 
 
 class bsdf_flag(enum.IntFlag):
@@ -108,7 +108,7 @@ class BsdfModel:
 
     def __init__(self, name, *args, **kwargs):
         lib = _lib.load()
-        if name not in ATTRIBUTES:
+        if name not in ATTRIBUTES and name not in AGGREGATES:
             raise ValueError(f"unknown BSDF model: {name}")
         mid = lib.bbm_hip_model_id(name.encode())
         if mid < 0:
@@ -116,6 +116,17 @@ class BsdfModel:
         self.name = name
         self.model_id = mid
         self._params = _model_params(mid, 0)
+        if name in AGGREGATES:
+            # Aggregate(child, child): children given as models (aggregatemodel.h:33, aggregate() :232-233)
+            if kwargs or (args and len(args) != len(AGGREGATES[name])):
+                raise TypeError(f"{name}: expected {len(AGGREGATES[name])} child models")
+            k = 0
+            for c, child in zip(AGGREGATES[name], args):
+                if child.name != c:
+                    raise TypeError(f"{name}: expected a {c} child, got {child.name}")
+                self._params[k:k + child._params.size] = child._params
+                k += child._params.size
+            return
         layout = ATTRIBUTES[name]
         if len(args) > len(layout):
             raise TypeError(f"{name}: too many positional attributes")
@@ -153,9 +164,38 @@ class BsdfModel:
         v = self._params[k:k + attr_size(shape)].copy()
         return v[0] if shape == () else v.reshape(shape)
 
-    def parameter_values(self):
-        """Flat parameter vector (bbm::parameter_values, include/bbm/bsdf_enumerate.h)."""
-        return self._params.copy()
+    def parameter_values(self, flag=None):
+        """Flat parameter vector (bbm::parameter_values, include/bbm/bsdf_enumerate.h:103-131).
+        flag=None: every parameter (the layout the kernels take, Dependent ones included);
+        flag=bsdf_attr bits: only the parameters whose attribute flags intersect it (the reference's
+        default bsdf_attr::All = 0x0F leaves out Dependent attributes)."""
+        if flag is None:
+            return self._params.copy()
+        return self._params[self.parameter_indices(flag)].copy()
+
+    def parameter_attrs(self):
+        """Per-parameter bsdf_attr flags (bbm_hip_model_param_attrs)."""
+        lib = _lib.load()
+        k = self._params.size
+        buf = (ctypes.c_uint32 * max(k, 1))()
+        _lib.check(lib.bbm_hip_model_param_attrs(self.model_id, buf, k))
+        return np.array(buf[:k], dtype=np.uint32)
+
+    def parameter_indices(self, flag=0x0F):
+        """Indices into the full parameter vector selected by parameter_values(flag)."""
+        return np.nonzero(self.parameter_attrs() & np.uint32(flag))[0]
+
+    def children(self):
+        """Aggregate: the child models (copies); otherwise []."""
+        if self.name not in AGGREGATES:
+            return []
+        out, k = [], 0
+        for c in AGGREGATES[self.name]:
+            m = BsdfModel(c)
+            m._params[:] = self._params[k:k + m._params.size]
+            k += m._params.size
+            out.append(m)
+        return out
 
     def set_parameter_values(self, values):
         v = np.asarray(values, dtype=np.float32).reshape(-1)
@@ -240,6 +280,18 @@ class BsdfModel:
                                       _stream_ptr(stream)))
         return BsdfSample(d, p, f)
 
+    def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
+        """Spectrum reflectance(out, component, unit, mask) for N directions -> (3, N) RGB."""
+        torch = _torch()
+        ox, oy, oz, n = _soa(out, what="out")
+        mptr, _keep = _mask_ptr(mask, n)
+        rgb = torch.empty((3, n), dtype=torch.float32, device=out.device)
+        lib = _lib.load()
+        _lib.check(lib.bbm_hip_reflectance(self.model_id, self._pptr(), self._params.size, ox, oy, oz, mptr, n,
+                                           int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),
+                                           rgb[2].data_ptr(), _stream_ptr(stream)))
+        return rgb
+
 
 # ------------------------------------------------------------------------- string import
 
@@ -270,20 +322,29 @@ def _parse_value(tok, i):
     return float(tok[i]), i + 1
 
 
-def fromString(s):
-    """Construct a model from its bbm::toString form, e.g. 'CookTorrance(albedo = [0.5, 0.5, 0.5],
-    roughness = 0.1, eta = 1.3)' (bsdf_string_convert.h:52-82 / bsdf_import.h:22-26).  Attributes
-    may appear in any order; missing ones keep their defaults."""
-    tok = _tokenize(s)
-    name = tok[0]
+def _parse_model(tok, i, s):
+    """Parse `Name(...)` starting at tok[i]; returns (model, next index)."""
+    name = tok[i]
+    if name == "Aggregate":
+        # Aggregate(child, child) (aggregatemodel.h:184-212)
+        if i + 1 >= len(tok) or tok[i + 1] != "(":
+            raise ValueError(f"malformed BSDF string: {s!r}")
+        kids, i = [], i + 2
+        while tok[i] != ")":
+            m, i = _parse_model(tok, i, s)
+            kids.append(m)
+            if tok[i] == ",":
+                i += 1
+        key = aggregate_key([k.name for k in kids])
+        if key not in AGGREGATES:
+            raise ValueError(f"unsupported aggregate: {key}")
+        return BsdfModel(key, *kids), i + 1
     if name not in ATTRIBUTES:
         raise ValueError(f"unknown BSDF model: {name}")
     m = BsdfModel(name)
-    if len(tok) == 1:
-        return m
-    if tok[1] != "(" or tok[-1] != ")":
-        raise ValueError(f"malformed BSDF string: {s!r}")
-    i, layout, pos_idx = 2, [a for a, _ in ATTRIBUTES[name]], 0
+    if i + 1 >= len(tok) or tok[i + 1] != "(":
+        return m, i + 1
+    i, layout, pos_idx = i + 2, [a for a, _ in ATTRIBUTES[name]], 0
     while tok[i] != ")":
         if i + 1 < len(tok) and tok[i + 1] == "=":
             attr = tok[i]
@@ -295,17 +356,38 @@ def fromString(s):
         m.set_attribute(attr, np.asarray(v, dtype=np.float32))
         if tok[i] == ",":
             i += 1
+    return m, i + 1
+
+
+def fromString(s):
+    """Construct a model from its bbm::toString form, e.g. 'CookTorrance(albedo = [0.5, 0.5, 0.5],
+    roughness = 0.1, eta = 1.3)' or 'Aggregate(Lambertian(...), Bagher(...))'
+    (bsdf_string_convert.h:52-82 / bsdf_import.h:22-26).  Attributes may appear in any order;
+    missing ones keep their defaults."""
+    tok = _tokenize(s)
+    m, i = _parse_model(tok, 0, s)
+    if i != len(tok):
+        raise ValueError(f"malformed BSDF string: {s!r}")
     return m
 
 
 bsdf_import = fromString
 
 
+def Aggregate(*children):
+    """aggregate(models...) (aggregatemodel.h:232-233) for the supported Aggregate(Lambertian, X) forms."""
+    key = aggregate_key([c.name for c in children])
+    if key not in AGGREGATES:
+        raise ValueError(f"unsupported aggregate: {key}")
+    return BsdfModel(key, *children)
+
+
 def _make_ctor(name):
     def ctor(*args, **kwargs):
         return BsdfModel(name, *args, **kwargs)
     ctor.__name__ = name
-    ctor.__doc__ = f"Constructs: {name}({', '.join(a for a, _ in ATTRIBUTES[name])}) -- {nparams(name)} parameters"
+    if name in ATTRIBUTES:
+        ctor.__doc__ = f"Constructs: {name}({', '.join(a for a, _ in ATTRIBUTES[name])}) -- {nparams(name)} parameters"
     return ctor
 
 

@@ -1,0 +1,103 @@
+// bbm_amd/csrc/aggregate.hpp -- aggregatemodel<A, B> (include/bsdfmodel/aggregatemodel.h:22-233):
+// the sum of two models, the form of every published fit (fits/*.fit: Aggregate(Lambertian(...),
+// X(...))).  Parameters are A's vector followed by B's (reflection order of the base classes).
+//   eval        = A.eval + B.eval                                            (:61-64)
+//   pdf         = (w_A pdf_A + w_B pdf_B) / (w_A + w_B), w = hsum(reflectance(out)), 0 if sum <= eps (:129-143)
+//   sample      = pick A or B by xi0 * sum against w_A, rescale xi0, sample it; pdf as above (:81-113)
+//   reflectance = A.reflectance + B.reflectance                              (:156-163)
+#pragma once
+#include "math.hpp"
+#include "microfacet.hpp"
+
+namespace bbmhip {
+
+template<class A, class B>
+struct Aggregate
+{
+  static constexpr int kParams = A::kParams + B::kParams;
+  static constexpr uint32_t kComponent = A::kComponent | B::kComponent;
+  A a;
+  B b;
+  __device__ explicit Aggregate(const float* p) : a(p), b(p + A::kParams) {}
+
+  // hsum(reflectance(out)) per child: std::accumulate from Value(0) (horizontal.h:64-67)
+  __device__ __forceinline__ void weights(v3 out, uint32_t component, float& wa, float& wb) const
+  {
+    float ra[3], rb[3];
+    a.reflectance(out, component, ra);
+    b.reflectance(out, component, rb);
+    wa = ((0.0f + ra[0]) + ra[1]) + ra[2];
+    wb = ((0.0f + rb[0]) + rb[1]) + rb[2];
+  }
+
+  // inner_product(pdfs, weights, Value(0)) / sum, masked sum > eps (:141-142)
+  __device__ __forceinline__ static float mix(float pa, float pb, float wa, float wb)
+  {
+    const float sum = (0.0f + wa) + wb;
+    const float ip = (0.0f + pa * wa) + pb * wb;
+    return (sum > kEpsF) ? div_nr(ip, sum) : 0.0f;
+  }
+
+  template<int MODE>
+  __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
+  {
+    float ra[3], rb[3], pa, pb;
+    a.template eval_pdf<MODE>(in, out, component, ra, pa);
+    b.template eval_pdf<MODE>(in, out, component, rb, pb);
+    rgb[0] = ra[0] + rb[0];
+    rgb[1] = ra[1] + rb[1];
+    rgb[2] = ra[2] + rb[2];
+    if (MODE & kModePdf)
+    {
+      float wa, wb;
+      weights(out, component, wa, wb);
+      pdf = component ? mix(pa, pb, wa, wb) : 0.0f;
+    }
+    else pdf = 0.0f;
+  }
+
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    float ra[3], rb[3];
+    a.reflectance(out, component, ra);
+    b.reflectance(out, component, rb);
+    rgb[0] = ra[0] + rb[0];
+    rgb[1] = ra[1] + rb[1];
+    rgb[2] = ra[2] + rb[2];
+  }
+
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f);
+    pdf = 0.0f;
+    flag = kFlagNone;
+    if (!component) return;   // masked lane: the reference returns {0, 0, None}
+    float wa, wb;
+    weights(out, component, wa, wb);
+    const float sum = (0.0f + wa) + wb;
+    float x = xi0 * sum;
+    // CONSTFOREACH over the children in order; a later child that also claims x overrides (:95-108)
+    const bool ma = (x >= 0) && (x <= wa);
+    if (ma)
+    {
+      const float nx = (wa > kEpsF) ? div_nr(x, wa) : 0.0f;
+      float p;
+      a.sample(out, nx, xi1, component, dir, p, flag);
+    }
+    x -= wa;
+    const bool mb = (x >= 0) && (x <= wb);
+    if (mb)
+    {
+      const float nx = (wb > kEpsF) ? div_nr(x, wb) : 0.0f;
+      float p;
+      b.sample(out, nx, xi1, component, dir, p, flag);
+    }
+    float rgb[3], pa, pb;
+    a.template eval_pdf<kModePdf>(dir, out, component, rgb, pa);
+    b.template eval_pdf<kModePdf>(dir, out, component, rgb, pb);
+    pdf = mix(pa, pb, wa, wb);
+  }
+};
+
+}  // namespace bbmhip

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/bbm_hip.h"
 #include "kernels.hpp"
@@ -26,6 +27,7 @@ BBM_HIP_MICROFACET_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_LOBE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_DIFFUSE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_SPECTRAL_MODELS(BBM_HIP_EXTERN)
+BBM_HIP_AGGREGATE_MODELS(BBM_HIP_EXTERN)
 
 namespace {
 
@@ -38,9 +40,14 @@ struct ModelEntry
   uint32_t components;
   EvalLauncher eval_pdf;
   SampleLauncher sample;
+  ReflLauncher reflectance;
+  LossLauncher loss;
   float defaults[kMaxParams];
   float lower[kMaxParams];
   float upper[kMaxParams];
+  // per-parameter bsdf_attr flags (include/bbm/bsdf_attr_flag.h:16-29), one letter per parameter:
+  // d DiffuseScale, D DiffuseParameter, s SpecularScale, p SpecularParameter, x Dependent
+  const char* attrs;
 };
 
 constexpr float kFMax = 3.4028234663852886e+38f;
@@ -49,74 +56,74 @@ constexpr float kFMin = 1.1754943508222875e-38f;
 // Defaults and bounds: bsdf_attribute.h:73-94 (scale 0.5 in [0,1], roughness 0.1 in [0,1] as
 // reported by parameter_lower_bound/upper_bound, ior 1.3 in [1,5]); pinned against
 // tests/golden/models.json by tests/test_abi.py.
-const ModelEntry kModels[] = {
-  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>, &launch_sample<Lambertian>,
-   {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}},
-  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>,   // bsdfmodel/low.h:32-33
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>, &launch_sample<GGXM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}},
-  {"CookTorranceHeitz", 6, kFlagSpecular, &launch_eval_pdf<CookTorranceHeitzM>, &launch_sample<CookTorranceHeitzM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}},
-  {"GGXHeitz", 6, kFlagSpecular, &launch_eval_pdf<GGXHeitzM>, &launch_sample<GGXHeitzM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}},
-  {"NganCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<NganCookTorranceM>, &launch_sample<NganCookTorranceM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, 0}, {1, 1, 1, 1, 1}},
-  {"PhongWalter", 5, kFlagSpecular, &launch_eval_pdf<PhongWalterM>, &launch_sample<PhongWalterM>,
-   {0.5f, 0.5f, 0.5f, 32.0f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, kFMax, 5}},
-  {"Ribardiere", 6, kFlagSpecular, &launch_eval_pdf<RibardiereM>, &launch_sample<RibardiereM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 40, 5}},
-  {"RibardiereAnisotropic", 7, kFlagSpecular, &launch_eval_pdf<RibardiereAnisoM>, &launch_sample<RibardiereAnisoM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 1, 40, 5}},
-  {"OrenNayar", 4, kFlagDiffuse, &launch_eval_pdf<OrenNayar>, &launch_sample<OrenNayar>,
-   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}},
-  {"LowMicrofacet", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>,
-   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}},
-  {"LowMicrofacetFit", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>,
-   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}},
-  {"Ward", 5, kFlagSpecular, &launch_eval_pdf<WardM>, &launch_sample<WardM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}},
-  {"WardDuer", 5, kFlagSpecular, &launch_eval_pdf<WardDuerM>, &launch_sample<WardDuerM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}},
-  {"WardDuerGeislerMoroder", 5, kFlagSpecular, &launch_eval_pdf<WardDGMM>, &launch_sample<WardDGMM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}},
-  {"NganWard", 4, kFlagSpecular, &launch_eval_pdf<NganWardM>, &launch_sample<NganWardM>,
-   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}},
-  {"NganWardDuer", 4, kFlagSpecular, &launch_eval_pdf<NganWardDuerM>, &launch_sample<NganWardDuerM>,
-   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}},
-  {"Phong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>,
-   {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}},
-  {"NganBlinnPhong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>,   // ngan.h:43-44
-   {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}},
-  {"Lafortune", 7, kFlagSpecular, &launch_eval_pdf<LafortuneM>, &launch_sample<LafortuneM>,
+const ModelEntry kSingle[] = {
+  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>, &launch_sample<Lambertian>, &launch_reflectance<Lambertian>, &launch_loss<Lambertian>,
+   {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}, "ddd"},
+  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
+  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>,   // bsdfmodel/low.h:32-33
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
+  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>, &launch_sample<GGXM>, &launch_reflectance<GGXM>, &launch_loss<GGXM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
+  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>, &launch_reflectance<CookTorranceWalterM>, &launch_loss<CookTorranceWalterM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
+  {"CookTorranceHeitz", 6, kFlagSpecular, &launch_eval_pdf<CookTorranceHeitzM>, &launch_sample<CookTorranceHeitzM>, &launch_reflectance<CookTorranceHeitzM>, &launch_loss<CookTorranceHeitzM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}, "sssppp"},
+  {"GGXHeitz", 6, kFlagSpecular, &launch_eval_pdf<GGXHeitzM>, &launch_sample<GGXHeitzM>, &launch_reflectance<GGXHeitzM>, &launch_loss<GGXHeitzM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}, "sssppp"},
+  {"NganCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<NganCookTorranceM>, &launch_sample<NganCookTorranceM>, &launch_reflectance<NganCookTorranceM>, &launch_loss<NganCookTorranceM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, 0}, {1, 1, 1, 1, 1}, "ssspp"},
+  {"PhongWalter", 5, kFlagSpecular, &launch_eval_pdf<PhongWalterM>, &launch_sample<PhongWalterM>, &launch_reflectance<PhongWalterM>, &launch_loss<PhongWalterM>,
+   {0.5f, 0.5f, 0.5f, 32.0f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, kFMax, 5}, "ssspp"},
+  {"Ribardiere", 6, kFlagSpecular, &launch_eval_pdf<RibardiereM>, &launch_sample<RibardiereM>, &launch_reflectance<RibardiereM>, &launch_loss<RibardiereM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 40, 5}, "sssppp"},
+  {"RibardiereAnisotropic", 7, kFlagSpecular, &launch_eval_pdf<RibardiereAnisoM>, &launch_sample<RibardiereAnisoM>, &launch_reflectance<RibardiereAnisoM>, &launch_loss<RibardiereAnisoM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 1, 40, 5}, "ssspppp"},
+  {"OrenNayar", 4, kFlagDiffuse, &launch_eval_pdf<OrenNayar>, &launch_sample<OrenNayar>, &launch_reflectance<OrenNayar>, &launch_loss<OrenNayar>,
+   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "dddD"},
+  {"LowMicrofacet", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>,
+   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
+  {"LowMicrofacetFit", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>,
+   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
+  {"Ward", 5, kFlagSpecular, &launch_eval_pdf<WardM>, &launch_sample<WardM>, &launch_reflectance<WardM>, &launch_loss<WardM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
+  {"WardDuer", 5, kFlagSpecular, &launch_eval_pdf<WardDuerM>, &launch_sample<WardDuerM>, &launch_reflectance<WardDuerM>, &launch_loss<WardDuerM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
+  {"WardDuerGeislerMoroder", 5, kFlagSpecular, &launch_eval_pdf<WardDGMM>, &launch_sample<WardDGMM>, &launch_reflectance<WardDGMM>, &launch_loss<WardDGMM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
+  {"NganWard", 4, kFlagSpecular, &launch_eval_pdf<NganWardM>, &launch_sample<NganWardM>, &launch_reflectance<NganWardM>, &launch_loss<NganWardM>,
+   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "sssp"},
+  {"NganWardDuer", 4, kFlagSpecular, &launch_eval_pdf<NganWardDuerM>, &launch_sample<NganWardDuerM>, &launch_reflectance<NganWardDuerM>, &launch_loss<NganWardDuerM>,
+   {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "sssp"},
+  {"Phong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>,
+   {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}, "sssp"},
+  {"NganBlinnPhong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>,   // ngan.h:43-44
+   {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}, "sssp"},
+  {"Lafortune", 7, kFlagSpecular, &launch_eval_pdf<LafortuneM>, &launch_sample<LafortuneM>, &launch_reflectance<LafortuneM>, &launch_loss<LafortuneM>,
    {0.5f, 0.5f, 0.5f, -0.57735026919f, -0.57735026919f, 0.57735026919f, 32.0f},
-   {0, 0, 0, kFMin, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax, kFMax}},
-  {"NganLafortune", 6, kFlagSpecular, &launch_eval_pdf<NganLafortuneM>, &launch_sample<NganLafortuneM>,
-   {0.5f, 0.5f, 0.5f, -0.57735026919f, 0.57735026919f, 32.0f}, {0, 0, 0, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax}},
-  {"AshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<ASM>, &launch_sample<ASM>,
-   {0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, kFMax, kFMax}},
-  {"AshikhminShirleyFull", 8, kFlagAll, &launch_eval_pdf<ASFullM>, &launch_sample<ASFullM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0, 0, 0, 0}, {1, 1, 1, 1, 1, 1, kFMax, kFMax}},
-  {"LowAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<LowASM>, &launch_sample<LowASM>,
-   {0.5f, 0.5f, 0.5f, 1.3f, 32.0f}, {0, 0, 0, 1, 0}, {1, 1, 1, 5, kFMax}},
-  {"NganAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<NganASM>, &launch_sample<NganASM>,
-   {0.5f, 0.5f, 0.5f, 0.1f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, 1, kFMax}},
-  {"LowSmooth", 6, kFlagSpecular, &launch_eval_pdf<LowSmooth>, &launch_sample<LowSmooth>,
-   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}},
+   {0, 0, 0, kFMin, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax, kFMax}, "ssspppp"},
+  {"NganLafortune", 6, kFlagSpecular, &launch_eval_pdf<NganLafortuneM>, &launch_sample<NganLafortuneM>, &launch_reflectance<NganLafortuneM>, &launch_loss<NganLafortuneM>,
+   {0.5f, 0.5f, 0.5f, -0.57735026919f, 0.57735026919f, 32.0f}, {0, 0, 0, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax}, "sssppp"},
+  {"AshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<ASM>, &launch_sample<ASM>, &launch_reflectance<ASM>, &launch_loss<ASM>,
+   {0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, kFMax, kFMax}, "ppppp"},
+  {"AshikhminShirleyFull", 8, kFlagAll, &launch_eval_pdf<ASFullM>, &launch_sample<ASFullM>, &launch_reflectance<ASFullM>, &launch_loss<ASFullM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0, 0, 0, 0}, {1, 1, 1, 1, 1, 1, kFMax, kFMax}, "dddppppp"},
+  {"LowAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<LowASM>, &launch_sample<LowASM>, &launch_reflectance<LowASM>, &launch_loss<LowASM>,
+   {0.5f, 0.5f, 0.5f, 1.3f, 32.0f}, {0, 0, 0, 1, 0}, {1, 1, 1, 5, kFMax}, "ssspp"},
+  {"NganAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<NganASM>, &launch_sample<NganASM>, &launch_reflectance<NganASM>, &launch_loss<NganASM>,
+   {0.5f, 0.5f, 0.5f, 0.1f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, 1, kFMax}, "ssspp"},
+  {"LowSmooth", 6, kFlagSpecular, &launch_eval_pdf<LowSmooth>, &launch_sample<LowSmooth>, &launch_reflectance<LowSmooth>, &launch_loss<LowSmooth>,
+   {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
   // bsdfmodel/bagher.h:62-68: albedo, K, Lambda, c, theta0, k (ndf/sgd.h:197-203, Dependent),
   // alpha, p (sgd.h:107-111), eta = (F0, F1) RGB (bagher.h:31, default {1, 0}, lower {0, -1})
-  {"Bagher", 30, kFlagSpecular, &launch_eval_pdf<Bagher>, &launch_sample<Bagher>,
+  {"Bagher", 30, kFlagSpecular, &launch_eval_pdf<Bagher>, &launch_sample<Bagher>, &launch_reflectance<Bagher>, &launch_loss<Bagher>,
    {0.5f, 0.5f, 0.5f, 7.5f, 7.5f, 7.5f, 1, 1, 1, 1, 1, 1, 1.5707963705062866f, 1.5707963705062866f, 1.5707963705062866f,
     1, 1, 1, 0.1f, 0.1f, 0.1f, 0.64f, 0.64f, 0.64f, 1, 1, 1, 0, 0, 0},
    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, kEpsF, kEpsF, kEpsF, 0, 0, 0, 0, 0, 0, -1, -1, -1},
    {1, 1, 1, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax,
-    1, 1, 1, kFMax, kFMax, kFMax, 1, 1, 1, 1, 1, 1}},
+    1, 1, 1, kFMax, kFMax, kFMax, 1, 1, 1, 1, 1, 1}, "sssxxxxxxxxxxxxxxxpppppppppppp"},
 };
-constexpr int kNumModels = int(sizeof(kModels) / sizeof(kModels[0]));
+constexpr int kNumSingle = int(sizeof(kSingle) / sizeof(kSingle[0]));
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
               CookTorranceHeitzM::kParams == 6 && GGXHeitzM::kParams == 6 && NganCookTorranceM::kParams == 5 &&
               PhongWalterM::kParams == 5 && RibardiereM::kParams == 6 && RibardiereAnisoM::kParams == 7 &&
@@ -125,7 +132,85 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 && NganASM::kParams == 5 &&
               LowSmooth::kParams == 6 && Bagher::kParams == 30, "registry nparams must match the compositions");
 
-const ModelEntry* entry(int id) { return (id >= 0 && id < kNumModels) ? &kModels[id] : nullptr; }
+// Aggregate(Lambertian, X) (aggregatemodel.h:22-233): parameters, defaults, bounds and attribute
+// flags are Lambertian's followed by X's; `child` names the registry entry X.
+struct AggregateSpec
+{
+  const char* name;
+  const char* child;
+  uint32_t components;
+  EvalLauncher eval_pdf;
+  SampleLauncher sample;
+  ReflLauncher reflectance;
+  LossLauncher loss;
+};
+#define BBM_HIP_AGG(KEY, CHILD, M) \
+  {KEY, CHILD, kFlagDiffuse | M::kComponent, &launch_eval_pdf<M>, &launch_sample<M>, &launch_reflectance<M>, &launch_loss<M>}
+const AggregateSpec kAggregates[] = {
+  BBM_HIP_AGG("Aggregate<Lambertian,Bagher>", "Bagher", AggBagherM),                      // fits/bagher_sgd.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,CookTorrance>", "CookTorrance", AggCookTorranceM),    // docs/source/fitting.rst:31-33
+  BBM_HIP_AGG("Aggregate<Lambertian,GGX>", "GGX", AggGGXM),
+  BBM_HIP_AGG("Aggregate<Lambertian,LowCookTorrance>", "LowCookTorrance", AggCookTorranceM),   // fits/low_cooktorrance_E*.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,LowAshikhminShirley>", "LowAshikhminShirley", AggLowASM),  // fits/low_ashikhminshirley_E*.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,LowMicrofacetFit>", "LowMicrofacetFit", AggLowMicrofacetM),  // fits/low_lowmicrofacet_E2.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,LowSmooth>", "LowSmooth", AggLowSmoothM),             // fits/low_lowsmooth_E2.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganAshikhminShirley>", "NganAshikhminShirley", AggNganASM),  // fits/ngan_ashikhminshirley.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganBlinnPhong>", "NganBlinnPhong", AggPhongM),       // fits/ngan_blinnphong.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganCookTorrance>", "NganCookTorrance", AggNganCookTorranceM),  // fits/ngan_cooktorrance.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganLafortune>", "NganLafortune", AggNganLafortuneM),  // fits/ngan_lafortune.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganWard>", "NganWard", AggNganWardM),                 // fits/ngan_ward.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganWardDuer>", "NganWardDuer", AggNganWardDuerM),     // fits/ngan_wardduer.fit
+};
+
+const ModelEntry* single(const char* name)
+{
+  for (const auto& e : kSingle)
+    if (std::strcmp(e.name, name) == 0) return &e;
+  return nullptr;
+}
+
+struct Registry
+{
+  std::vector<ModelEntry> models;
+  std::vector<std::string> attrs;   // storage for the aggregates' attribute strings
+  Registry()
+  {
+    models.assign(kSingle, kSingle + kNumSingle);
+    const ModelEntry* lam = single("Lambertian");
+    attrs.reserve(sizeof(kAggregates) / sizeof(kAggregates[0]));
+    for (const auto& g : kAggregates)
+    {
+      const ModelEntry* c = single(g.child);
+      ModelEntry e{};
+      e.name = g.name;
+      e.nparams = lam->nparams + c->nparams;
+      e.components = g.components;
+      e.eval_pdf = g.eval_pdf; e.sample = g.sample; e.reflectance = g.reflectance; e.loss = g.loss;
+      for (int i = 0; i < lam->nparams; ++i)
+      {
+        e.defaults[i] = lam->defaults[i]; e.lower[i] = lam->lower[i]; e.upper[i] = lam->upper[i];
+      }
+      for (int i = 0; i < c->nparams; ++i)
+      {
+        e.defaults[lam->nparams + i] = c->defaults[i];
+        e.lower[lam->nparams + i] = c->lower[i];
+        e.upper[lam->nparams + i] = c->upper[i];
+      }
+      attrs.push_back(std::string(lam->attrs) + c->attrs);
+      e.attrs = attrs.back().c_str();
+      models.push_back(e);
+    }
+  }
+};
+
+const Registry& registry()
+{
+  static const Registry r;
+  return r;
+}
+
+int num_models() { return int(registry().models.size()); }
+const ModelEntry* entry(int id) { return (id >= 0 && id < num_models()) ? &registry().models[size_t(id)] : nullptr; }
 
 int prepare(int model_id, const float* params, int nparams, size_t n, EvalArgs& a, const ModelEntry*& e)
 {
@@ -177,7 +262,59 @@ __global__ __launch_bounds__(kBlock) void k_fill_dirs(uint64_t key, uint64_t off
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_linearize(LinDesc d, uint64_t begin, uint64_t n, float* __restrict__ ix,
+                                                      float* __restrict__ iy, float* __restrict__ iz, float* __restrict__ ox,
+                                                      float* __restrict__ oy, float* __restrict__ oz)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+  {
+    v3 in, out;
+    lin_pair(d, begin + i, in, out);
+    ix[i] = in.x; iy[i] = in.y; iz[i] = in.z;
+    ox[i] = out.x; oy[i] = out.y; oz[i] = out.z;
+  }
+}
+
+int to_desc(const bbm_hip_linearizer* lin, LinDesc& d)
+{
+  if (!lin) return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer is NULL");
+  if (lin->kind != kLinSpherical && lin->kind != kLinMerl)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer kind must be BBM_LIN_SPHERICAL or BBM_LIN_MERL");
+  std::memset(&d, 0, sizeof(d));
+  d.kind = lin->kind;
+  for (int k = 0; k < 2; ++k)
+  {
+    if (lin->samples_in[k] == 0 || lin->samples_out[k] == 0)
+      return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer sample counts must be positive");
+    d.s_in[k] = lin->samples_in[k];
+    d.s_out[k] = lin->samples_out[k];
+    d.start_in[k] = lin->start_in[k];
+    d.start_out[k] = lin->start_out[k];
+    d.size_in[k] = lin->end_in[k] - lin->start_in[k];      // _sizeIn(endIn - startIn), float
+    d.size_out[k] = lin->end_out[k] - lin->start_out[k];
+  }
+  return BBM_HIP_OK;
+}
+
 }  // namespace
+
+__global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums, int nblocks, int nprobes, double* sums)
+{
+  __shared__ double part[kBlock];
+  const int p = blockIdx.x;
+  double t = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) t += block_sums[size_t(b) * nprobes + p];
+  part[threadIdx.x] = t;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1)
+  {
+    if (int(threadIdx.x) < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[p] = part[0];
+}
+
 }  // namespace bbmhip
 
 using namespace bbmhip;
@@ -188,7 +325,7 @@ int bbm_hip_abi_version(void) { return BBM_HIP_ABI_VERSION; }
 
 const char* bbm_hip_last_error(void) { return g_last_error.c_str(); }
 
-int bbm_hip_num_models(void) { return kNumModels; }
+int bbm_hip_num_models(void) { return num_models(); }
 
 const char* bbm_hip_model_name(int model_id)
 {
@@ -199,8 +336,8 @@ const char* bbm_hip_model_name(int model_id)
 int bbm_hip_model_id(const char* name)
 {
   if (!name) return fail(BBM_HIP_ERR_INVALID_ARG, "name is NULL");
-  for (int i = 0; i < kNumModels; ++i)
-    if (std::strcmp(kModels[i].name, name) == 0) return i;
+  for (int i = 0; i < num_models(); ++i)
+    if (std::strcmp(registry().models[size_t(i)].name, name) == 0) return i;
   return fail(BBM_HIP_ERR_INVALID_MODEL, std::string("unknown BSDF model: ") + name);
 }
 
@@ -301,6 +438,113 @@ int bbm_hip_sample(int model_id, const float* params, int nparams,
   a.dx = dir_x; a.dy = dir_y; a.dz = dir_z; a.pdf = pdf; a.flag = flag;
   a.component = component & kFlagAll;
   return e->sample(a, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_reflectance(int model_id, const float* params, int nparams,
+                        const float* out_x, const float* out_y, const float* out_z,
+                        const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                        float* r, float* g, float* b, void* stream)
+{
+  (void)unit;
+  EvalArgs tmp;
+  const ModelEntry* e;
+  int rc = prepare(model_id, params, nparams, n, tmp, e);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if ((rc = check_dirs(out_x, out_y, out_z, "out"))) return rc;
+  if (!r || !g || !b) return fail(BBM_HIP_ERR_INVALID_ARG, "reflectance output pointer is NULL");
+  ReflArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = tmp.p;
+  a.n = n;
+  a.ox = out_x; a.oy = out_y; a.oz = out_z; a.mask = mask; a.r = r; a.g = g; a.b = b;
+  a.component = component & kFlagAll;
+  return e->reflectance(a, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_model_param_attrs(int model_id, uint32_t* out, int capacity)
+{
+  const ModelEntry* e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  for (int i = 0; out && i < e->nparams && i < capacity; ++i)
+  {
+    switch (e->attrs[i])
+    {
+      case 'd': out[i] = 0x01u; break;
+      case 'D': out[i] = 0x02u; break;
+      case 's': out[i] = 0x04u; break;
+      case 'p': out[i] = 0x08u; break;
+      default: out[i] = 0x10u; break;
+    }
+  }
+  return e->nparams;
+}
+
+int bbm_hip_linearizer_size(const bbm_hip_linearizer* lin, uint64_t* size)
+{
+  LinDesc d;
+  int rc = to_desc(lin, d);
+  if (rc) return rc;
+  if (!size) return fail(BBM_HIP_ERR_INVALID_ARG, "size is NULL");
+  *size = lin_size(d);
+  return BBM_HIP_OK;
+}
+
+int bbm_hip_linearize(const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
+                      float* in_x, float* in_y, float* in_z, float* out_x, float* out_y, float* out_z,
+                      void* stream)
+{
+  LinDesc d;
+  int rc = to_desc(lin, d);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if (begin + n > lin_size(d)) return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer range out of bounds");
+  if (!in_x || !in_y || !in_z || !out_x || !out_y || !out_z)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "direction pointer is NULL");
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipLaunchKernelGGL(k_linearize, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), d, begin,
+                     uint64_t(n), in_x, in_y, in_z, out_x, out_y, out_z);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+size_t bbm_hip_loss_workspace_size(int nprobes)
+{
+  return nprobes > 0 ? size_t(kLossMaxBlocks) * size_t(nprobes) * sizeof(double) : 0;
+}
+
+int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
+                 const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
+                 const float* ref_r, const float* ref_g, const float* ref_b,
+                 int loss_kind, uint32_t component, uint32_t unit,
+                 double* sums, void* workspace, size_t workspace_bytes, void* stream)
+{
+  (void)unit;
+  const ModelEntry* e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  if (nparams != e->nparams)
+    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
+                                             " parameters, got " + std::to_string(nparams));
+  if (nprobes <= 0) return fail(BBM_HIP_ERR_INVALID_ARG, "nprobes must be positive");
+  if (loss_kind < BBM_LOSS_NGAN_L2 || loss_kind > BBM_LOSS_BIERON_LOG) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown loss kind");
+  LossArgs a;
+  std::memset(&a, 0, sizeof(a));
+  int rc = to_desc(lin, a.lin);
+  if (rc) return rc;
+  if (begin + n > lin_size(a.lin)) return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer range out of bounds");
+  if (!probes || !sums) return fail(BBM_HIP_ERR_INVALID_ARG, "probes / sums pointer is NULL");
+  if (n > 0 && (!ref_r || !ref_g || !ref_b)) return fail(BBM_HIP_ERR_INVALID_ARG, "reference pointer is NULL");
+  if (!workspace || workspace_bytes < bbm_hip_loss_workspace_size(nprobes))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "workspace too small (bbm_hip_loss_workspace_size)");
+  a.begin = begin; a.n = n;
+  a.ref_r = ref_r; a.ref_g = ref_g; a.ref_b = ref_b;
+  a.probes = probes; a.nprobes = nprobes; a.stride = nparams; a.loss_kind = loss_kind;
+  a.component = component & kFlagAll;
+  a.block_sums = static_cast<double*>(workspace);
+  a.sums = sums;
+  return e->loss(a, static_cast<hipStream_t>(stream));
 }
 
 int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,

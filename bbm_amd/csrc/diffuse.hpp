@@ -24,6 +24,13 @@ struct Lambertian
     pdf = m ? in.z * kInvPiF : 0.0f;
   }
 
+  // lambertian.h:136-140: albedo for the Diffuse component (no horizon test)
+  __device__ __forceinline__ void reflectance(v3, uint32_t component, float* rgb) const
+  {
+    const bool m = component & kFlagDiffuse;
+    rgb[0] = m ? albedo[0] : 0.0f; rgb[1] = m ? albedo[1] : 0.0f; rgb[2] = m ? albedo[2] : 0.0f;
+  }
+
   // lambertian.h:76-103 cosine-weighted sampling; sinTheta = safe_sqrt(1.0 - xi1) in double
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
                                          uint32_t& flag) const
@@ -50,9 +57,10 @@ struct OrenNayar
 {
   static constexpr int kParams = 4;
   static constexpr uint32_t kComponent = kFlagDiffuse;
-  float alb_pi[3], A, B;
+  float albedo[3], alb_pi[3], A, B;
   __device__ explicit OrenNayar(const float* p)
   {
+    albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2];
     const float sigma2 = p[3] * p[3];
     A = float(1 - 0.5 * sigma2 / (sigma2 + 0.33));
     B = float(0.45 * sigma2 / (sigma2 + 0.09));
@@ -73,6 +81,13 @@ struct OrenNayar
     rgb[1] = m ? alb_pi[1] * factor : 0.0f;
     rgb[2] = m ? alb_pi[2] * factor : 0.0f;
     pdf = (diff && (in.z >= 0) && (out.z >= 0)) ? in.z * kInvPiF : 0.0f;
+  }
+
+  // orennayar.h:131-135: albedo for the Diffuse component
+  __device__ __forceinline__ void reflectance(v3, uint32_t component, float* rgb) const
+  {
+    const bool m = component & kFlagDiffuse;
+    rgb[0] = m ? albedo[0] : 0.0f; rgb[1] = m ? albedo[1] : 0.0f; rgb[2] = m ? albedo[2] : 0.0f;
   }
 
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,

@@ -19,6 +19,7 @@
 #include "../../include/bbm_hip.h"
 #include "math.hpp"
 #include "microfacet.hpp"
+#include "fit.hpp"
 
 namespace bbmhip {
 
@@ -431,7 +432,135 @@ int launch_eval_pdf(const EvalArgs& a, int mode, hipStream_t s)
   }
 }
 
+// ------------------------------------------------------------------------- reflectance
+
+struct ReflArgs
+{
+  const float* ox; const float* oy; const float* oz;
+  const uint8_t* mask;
+  float* r; float* g; float* b;
+  uint64_t n;
+  uint32_t component;
+  ParamBlock p;
+};
+
+// bsdfmodel::reflectance per direction (not on the headline path: one scalar lane per direction)
+template<class Model>
+__global__ __launch_bounds__(kBlock) void k_reflectance(ReflArgs a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+  {
+    float rgb[3];
+    const bool active = a.mask ? (a.mask[i] != 0) : true;
+    m.reflectance(mk3(a.ox[i], a.oy[i], a.oz[i]), active ? a.component : 0u, rgb);
+    a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2];
+  }
+}
+
+template<class Model>
+int launch_reflectance(const ReflArgs& a, hipStream_t s)
+{
+  uint64_t blocks = (a.n + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > max_blocks()) blocks = max_blocks();
+  hipLaunchKernelGGL((k_reflectance<Model>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+// ------------------------------------------------------------------------- fitting loss
+
+constexpr int kProbeBatch = 8;          // probes evaluated per pass over the samples (f64 accumulators)
+constexpr int kLossMaxBlocks = 2048;    // workspace = kLossMaxBlocks x nprobes doubles
+
+struct LossArgs
+{
+  LinDesc lin;
+  uint64_t begin, n;                    // samples [begin, begin + n) of the linearizer
+  const float* ref_r; const float* ref_g; const float* ref_b;   // reference value of sample begin + i
+  const float* probes;                  // nprobes x stride parameter vectors (device)
+  int nprobes, stride, loss_kind;
+  uint32_t component;
+  double* block_sums;                   // [gridDim.x][nprobes]
+  double* sums;                         // [nprobes]
+};
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template<class Model>
+__global__ __launch_bounds__(kBlock) void k_loss(LossArgs a)
+{
+  __shared__ double part[kBlock / 64][kProbeBatch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (int p0 = 0; p0 < a.nprobes; p0 += kProbeBatch)
+  {
+    double acc[kProbeBatch];
+#pragma unroll
+    for (int j = 0; j < kProbeBatch; ++j) acc[j] = 0.0;
+    for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+    {
+      v3 in, out;
+      lin_pair(a.lin, a.begin + i, in, out);
+      const float ref[3] = {a.ref_r[i], a.ref_g[i], a.ref_b[i]};
+      const LossSample s = loss_prepare(a.loss_kind, in, out, ref);
+#pragma unroll
+      for (int j = 0; j < kProbeBatch; ++j)
+      {
+        if (p0 + j >= a.nprobes) break;           // uniform
+        const Model m(a.probes + size_t(p0 + j) * size_t(a.stride));
+        float rgb[3], pdf;
+        m.template eval_pdf<kModeEval>(in, out, a.component, rgb, pdf);
+        acc[j] += double(sample_loss(a.loss_kind, s, rgb));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kProbeBatch; ++j)
+    {
+      const double v = wave_sum(acc[j]);
+      if (lane == 0) part[wave][j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kProbeBatch && p0 + int(threadIdx.x) < a.nprobes)
+    {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) t += part[w][threadIdx.x];
+      a.block_sums[size_t(blockIdx.x) * a.nprobes + p0 + threadIdx.x] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// sums[p] = sum over blocks of block_sums[b][p], in block order (one workgroup per probe; fixed tree)
+__global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums, int nblocks, int nprobes, double* sums);
+
+template<class Model>
+int launch_loss(const LossArgs& a0, hipStream_t s)
+{
+  LossArgs a = a0;
+  uint64_t blocks = (a.n + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
+  hipLaunchKernelGGL((k_loss<Model>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_loss_final, dim3(unsigned(a.nprobes)), dim3(kBlock), 0, s, a.block_sums, int(blocks), a.nprobes,
+                     a.sums);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+using LossLauncher = int (*)(const LossArgs&, hipStream_t);
 using EvalLauncher = int (*)(const EvalArgs&, int, hipStream_t);
 using SampleLauncher = int (*)(const SampleArgs&, hipStream_t);
+using ReflLauncher = int (*)(const ReflArgs&, hipStream_t);
 
 }  // namespace bbmhip

@@ -95,6 +95,14 @@ struct Ward
   }
 
   // ward.h:67-93
+  // ward.h:151-155 (inherited by Ward-Duer variants): albedo for the Specular component
+  __device__ __forceinline__ void reflectance(v3, uint32_t component, float* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0f;
+  }
+
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
                                          uint32_t& flag) const
   {
@@ -135,6 +143,14 @@ struct PhongLobe
     rgb[1] = active ? albedo[1] * f : 0.0f;
     rgb[2] = active ? albedo[2] * f : 0.0f;
     pdf = active ? (s + 1) * kInvPiHalfF * pw : 0.0f;
+  }
+
+  // phong.h:145-149: albedo for the Specular component
+  __device__ __forceinline__ void reflectance(v3, uint32_t component, float* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0f;
   }
 
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
@@ -196,6 +212,18 @@ struct Lafortune
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;
+  }
+
+  // lafortune.h:151-156: albedo pow(|C out|, s) 2 pi / (s + 2) for the Specular component
+  // (no horizon test); NganLafortune masks the same way (ngan.h:109-121)
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+    const v3 co = mk3(cx * out.x, cy * out.y, cz * out.z);
+    const float nrm = powf(sqrtf(dot3(co, co)), s) * kPi2F;
+    const float normalization = div_nr(nrm, s + 2);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] * normalization : 0.0f;
   }
 
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
@@ -377,6 +405,27 @@ struct AshikhminShirley
     flag = kFlagSpecular;
   }
 
+  // ashikhminshirley.h:181-190 (Fresnel at z(out), Specular, z(out) > 0) [x albedo, scaledmodel.h:64-67];
+  // FULL: + diffuse (1 - fresnelReflectance) for the Diffuse component (ashikhminshirleyfull.h:170-185)
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool up = out.z > 0;
+    const bool ms = (component & kFlagSpecular) && up;
+    float F[3];
+    fres.eval3(out.z, F);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      float v = ms ? (SCALED ? F[c] * albedo[c] : F[c]) : 0.0f;
+      if constexpr (FULL)
+      {
+        const float d = diffuse[c] * (1.0f - fres.r0[c]);
+        v = (up && (component & kFlagDiffuse)) ? d + v : v;
+      }
+      rgb[c] = up ? v : 0.0f;
+    }
+  }
+
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
                                          uint32_t& flag) const
   {
@@ -448,6 +497,20 @@ struct LowSmooth
   }
 
   // lowsmooth.h:75-111
+  // lowsmooth.h:166-176: 2 pi A factor R0, Specular component and z(out) > 0.  factor's branches
+  // (log(B+1) / 2B in float; (1.0 - pow(B+1, 1-C)) / (2B(C-1)) in double) both rounded to float
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    const float f1 = div_nr(logf(B + 1), 2 * B);
+    const float f2 = float((1.0 - double(powf(B + 1, 1 - C))) / double(2 * B * (C - 1)));
+    const float factor = (fabsf(C - 1) < kEpsF) ? f1 : f2;
+    const float q = div_nr(fres.eta - 1, fres.eta + 1);
+    const float R0 = q * q;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? ((kPi2F * A[c]) * factor) * R0 : 0.0f;
+  }
+
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
                                          uint32_t& flag) const
   {

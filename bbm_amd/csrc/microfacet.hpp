@@ -473,6 +473,16 @@ struct Microfacet
     else pdf = 0.0f;
   }
 
+  // microfacet.h:182-196 reflectance: mirror approximation Fresnel(eta, z(out)) / N * 4.0 (double),
+  // x albedo (scaledmodel.h:64-67); Specular component and z(out) > 0, else 0.
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    const float f = float(double(fresnel.eval(out.z)) / norm_value<N>::v * 4.0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? (Scaled ? f * albedo[c] : f) : 0.0f;
+  }
+
   // microfacet.h:115-141 sample: m ~ VNDF(out), direction = reflect(out, m)
   // (core/vec_transform.h:43-44, `m * dot(m, out) * 2.0 - out`: the double subtraction of two float
   // values rounded to float is the float subtraction), pdf = microfacet pdf of that direction.

@@ -6,6 +6,7 @@
 #include "lobes.hpp"
 #include "microfacet.hpp"
 #include "spectral.hpp"
+#include "aggregate.hpp"
 
 namespace bbmhip {
 
@@ -34,6 +35,20 @@ using ASFullM = AshikhminShirley<FresnelSchlickRGB, true, false, true>;         
 using LowASM = AshikhminShirley<ScalarFresnel3<FresnelCook>, false, true, false>;          // bsdfmodel/low.h:24-25
 using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, false>;      // bsdfmodel/ngan.h:157-158
 
+// Aggregate(Lambertian, X): the form of every published fit (fits/*.fit), aggregatemodel.h:22-233
+using AggBagherM = Aggregate<Lambertian, Bagher>;
+using AggCookTorranceM = Aggregate<Lambertian, CookTorranceM>;
+using AggGGXM = Aggregate<Lambertian, GGXM>;
+using AggLowASM = Aggregate<Lambertian, LowASM>;
+using AggLowMicrofacetM = Aggregate<Lambertian, LowMicrofacetM>;
+using AggLowSmoothM = Aggregate<Lambertian, LowSmooth>;
+using AggNganASM = Aggregate<Lambertian, NganASM>;
+using AggPhongM = Aggregate<Lambertian, PhongLobe>;
+using AggNganCookTorranceM = Aggregate<Lambertian, NganCookTorranceM>;
+using AggNganLafortuneM = Aggregate<Lambertian, NganLafortuneM>;
+using AggNganWardM = Aggregate<Lambertian, NganWardM>;
+using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
+
 }  // namespace bbmhip
 
 // X(composition) per instantiation unit
@@ -45,10 +60,17 @@ using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, fa
   X(ASM) X(ASFullM) X(LowASM) X(NganASM) X(LowSmooth)
 #define BBM_HIP_DIFFUSE_MODELS(X) X(Lambertian) X(OrenNayar)
 #define BBM_HIP_SPECTRAL_MODELS(X) X(Bagher)
+#define BBM_HIP_AGGREGATE_MODELS(X) \
+  X(AggBagherM) X(AggCookTorranceM) X(AggGGXM) X(AggLowASM) X(AggLowMicrofacetM) X(AggLowSmoothM) X(AggNganASM) \
+  X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM)
 
 #define BBM_HIP_INSTANTIATE(M)                                                   \
   template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);           \
-  template int launch_sample<M>(const SampleArgs&, hipStream_t);
+  template int launch_sample<M>(const SampleArgs&, hipStream_t);                \
+  template int launch_reflectance<M>(const ReflArgs&, hipStream_t);            \
+  template int launch_loss<M>(const LossArgs&, hipStream_t);
 #define BBM_HIP_EXTERN(M)                                                        \
   extern template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);    \
-  extern template int launch_sample<M>(const SampleArgs&, hipStream_t);
+  extern template int launch_sample<M>(const SampleArgs&, hipStream_t);         \
+  extern template int launch_reflectance<M>(const ReflArgs&, hipStream_t);     \
+  extern template int launch_loss<M>(const LossArgs&, hipStream_t);

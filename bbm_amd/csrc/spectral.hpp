@@ -98,6 +98,21 @@ struct Bagher
     else pdf = 0.0f;
   }
 
+  // microfacet.h:182-196 with fresnel::bagher at cos = z(out), x albedo (scaledmodel.h:64-67)
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    const double x = double(1.0f - out.z);
+    const double x5 = (x * x) * (x * x) * x;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+    {
+      const float S = float(double(F0[j]) + double(1.0f - F0[j]) * x5);
+      const float F = S - F1[j] * out.z;
+      rgb[j] = m ? float(double(F) / kPiD * 4.0) * albedo[j] : 0.0f;
+    }
+  }
+
   // microfacet.h:115-141 with the GGX(avg alpha) visible-normal sampler
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
                                          uint32_t& flag) const

@@ -1,0 +1,251 @@
+"""Fitting on the GPU: linearizers, sampled losses and the compass search (BASELINE config 5).
+
+Host-side mirror of the reference's fitting layer (include/bbm/sampledlossfunction.h,
+include/loss/*.h, include/linearizer/*.h, include/optimizer/compass.h):
+
+* `spherical_linearizer` / `merl_linearizer` describe the (in, out) sample grid
+  (bbm_hip_linearizer, include/bbm_hip.h);
+* `SampledLoss(fitted, reference, loss, linearizer)` is sampledlossfunction: the mean of a
+  per-sample loss (nganL2 ... bieronLog) between the fitted model and a reference over the grid.
+  The reference is a table of RGB values on the grid (a measured material is a table); it can be
+  filled from a model on the GPU (`reference_table`).  `probe_losses(P)` evaluates many parameter
+  vectors in ONE kernel launch (bbm_hip_loss) -- the 2P probes of a compass step;
+* `Compass` is compass (compass.h:40-183) with the probes batched: the host reproduces the
+  reference's sequence of float parameter updates exactly (probe, restore by subtraction, box
+  test), the GPU scores all probes of the step at once, and the host applies the reference's
+  sequential "strictly better" rule to the scores.
+
+Multi-GPU (one process per GPU, torch.distributed): the sample grid is split into contiguous
+shards; every rank scores all probes on its shard and the per-probe sums are all-reduced (RCCL
+over xGMI, 2P doubles per step).  Every rank then takes the identical compass decision.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib
+from .backbone import _stream_ptr, _torch
+
+LIN_SPHERICAL, LIN_MERL = 0, 1
+NGAN_L2, LOW_L2, BIERON_L2, STANDARD_LOG, LOW_LOG, BIERON_LOG = range(6)
+LOSS_NAMES = {"nganL2": NGAN_L2, "lowL2": LOW_L2, "bieronL2": BIERON_L2, "standardLog": STANDARD_LOG,
+              "lowLog": LOW_LOG, "bieronLog": BIERON_LOG}
+ALL = 0x0F          # bsdf_attr::All (include/bbm/bsdf_attr_flag.h:27)
+
+_F32 = np.float32
+# constants<float>::Pi(scale) = T(scale * std::numbers::pi) (include/core/constants.h:16-24)
+PI = float(_F32(math.pi))
+HEMISPHERE = (float(_F32(2.0 * math.pi)), float(_F32(0.5 * math.pi)))
+EPSILON = float(np.finfo(np.float32).eps)
+
+
+class Linearizer(ctypes.Structure):
+    """bbm_hip_linearizer (include/bbm_hip.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("samples_in", ctypes.c_uint64 * 2), ("samples_out", ctypes.c_uint64 * 2),
+                ("start_in", ctypes.c_float * 2), ("end_in", ctypes.c_float * 2),
+                ("start_out", ctypes.c_float * 2), ("end_out", ctypes.c_float * 2)]
+
+    def size(self):
+        n = ctypes.c_uint64()
+        _lib.check(_lib.load().bbm_hip_linearizer_size(ctypes.byref(self), ctypes.byref(n)))
+        return int(n.value)
+
+    def directions(self, begin=0, n=None, stream=None):
+        """(in, out) direction pairs begin .. begin+n-1 -> two (3, n) float32 CUDA tensors."""
+        torch = _torch()
+        if n is None:
+            n = self.size() - begin
+        dev = torch.device("cuda", torch.cuda.current_device())
+        din = torch.empty((3, n), dtype=torch.float32, device=dev)
+        dout = torch.empty((3, n), dtype=torch.float32, device=dev)
+        _lib.check(_lib.load().bbm_hip_linearize(ctypes.byref(self), begin, n, din[0].data_ptr(), din[1].data_ptr(),
+                                                  din[2].data_ptr(), dout[0].data_ptr(), dout[1].data_ptr(),
+                                                  dout[2].data_ptr(), _stream_ptr(stream)))
+        return din, dout
+
+
+def spherical_linearizer(samples_in, samples_out, start_in=(0.0, 0.0), end_in=HEMISPHERE, start_out=(0.0, 0.0),
+                         end_out=HEMISPHERE):
+    """spherical_linearizer(samplesIn, samplesOut, startIn, endIn, startOut, endOut), all (phi, theta)
+    (include/linearizer/spherical_linearizer.h:38-45)."""
+    lin = Linearizer()
+    lin.kind = LIN_SPHERICAL
+    for k in range(2):
+        lin.samples_in[k], lin.samples_out[k] = int(samples_in[k]), int(samples_out[k])
+        lin.start_in[k], lin.end_in[k] = start_in[k], end_in[k]
+        lin.start_out[k], lin.end_out[k] = start_out[k], end_out[k]
+    return lin
+
+
+def merl_linearizer(h=(1, 90), d=(180, 90)):
+    """merl_linearizer(samplesH, samplesD) (include/linearizer/merl_linearizer.h:28)."""
+    lin = Linearizer()
+    lin.kind = LIN_MERL
+    for k in range(2):
+        lin.samples_in[k], lin.samples_out[k] = int(h[k]), int(d[k])
+    return lin
+
+
+def shard_range(total, rank, world):
+    """Contiguous shard [begin, end) of `total` samples for `rank` of `world` (balanced)."""
+    q, r = divmod(total, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
+def reference_table(model, lin, begin=0, n=None, stream=None):
+    """Reference values on the linearizer's samples begin .. begin+n-1: model.eval on the GPU
+    (Spectrum per sample, component All) -> (3, n) float32 CUDA tensor."""
+    din, dout = lin.directions(begin, n, stream)
+    return model.eval(din, dout, stream=stream)
+
+
+class SampledLoss:
+    """sampledlossfunction<fitted, reference, loss, linearizer> (include/bbm/sampledlossfunction.h:34-97).
+
+    fitted: a BsdfModel whose parameter layout the probes use; reference: a BsdfModel (evaluated
+    once into a table on this rank's shard) or a (3, n_shard) CUDA tensor of reference values.
+    dist: torch.distributed module (or None); the shard is this rank's part of the grid."""
+
+    def __init__(self, fitted, reference, loss, lin, component=3, unit=0, dist=None, stream=None):
+        torch = _torch()
+        self.fitted = fitted
+        self.loss_kind = LOSS_NAMES[loss] if isinstance(loss, str) else int(loss)
+        self.lin = lin
+        self.component, self.unit = int(component), int(unit)
+        self.dist = dist
+        self.stream = stream
+        self.total = lin.size()
+        rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+        self.begin, end = shard_range(self.total, rank, world)
+        self.n = end - self.begin
+        if hasattr(reference, "eval"):
+            self.ref = reference_table(reference, lin, self.begin, self.n, stream)
+        else:
+            self.ref = reference
+        if self.ref.shape != (3, self.n):
+            raise ValueError(f"reference table: expected shape (3, {self.n}), got {tuple(self.ref.shape)}")
+        self.dev = self.ref.device
+        self._ws = None
+        self._ws_probes = 0
+        self.launches = 0
+
+    def samples(self):
+        return self.total
+
+    def _workspace(self, nprobes):
+        torch = _torch()
+        if self._ws is None or self._ws_probes < nprobes:
+            nbytes = _lib.load().bbm_hip_loss_workspace_size(nprobes)
+            self._ws = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=self.dev)
+            self._ws_probes = nprobes
+        return self._ws
+
+    def probe_sums(self, probes):
+        """Per-probe loss sums over the WHOLE grid: this rank's shard (local_sums), then the
+        cross-rank all-reduce -- RCCL over xGMI, 2P doubles per compass step."""
+        sums = self.local_sums(probes)
+        if self.dist is not None and self.dist.get_world_size() > 1:
+            self.dist.all_reduce(sums)
+        return sums
+
+    def local_sums(self, probes):
+        """Per-probe loss sums over this rank's shard: one bbm_hip_loss launch -> float64 tensor (nprobes,)."""
+        torch = _torch()
+        p = np.ascontiguousarray(np.asarray(probes, dtype=np.float32).reshape(-1, self.fitted._params.size))
+        nprobes, npar = p.shape
+        dp = torch.from_numpy(p).to(self.dev, non_blocking=False)
+        sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
+        ws = self._workspace(nprobes)
+        _lib.check(_lib.load().bbm_hip_loss(self.fitted.model_id, dp.data_ptr(), npar, nprobes, ctypes.byref(self.lin),
+                                            self.begin, self.n, self.ref[0].data_ptr(), self.ref[1].data_ptr(),
+                                            self.ref[2].data_ptr(), self.loss_kind, self.component, self.unit,
+                                            sums.data_ptr(), ws.data_ptr(), ws.numel() * 8, _stream_ptr(self.stream)))
+        self.launches += 1
+        return sums
+
+    def probe_losses(self, probes):
+        """Mean loss per probe (err / numsamples, sampledlossfunction.h:80-87) as float32 values."""
+        s = self.probe_sums(probes).cpu().numpy()
+        return (s / float(self.total)).astype(np.float32)
+
+    def __call__(self, params=None):
+        """Loss of one parameter vector (the fitted model's current parameters by default)."""
+        p = self.fitted._params if params is None else params
+        return float(self.probe_losses(np.asarray(p, np.float32)[None])[0])
+
+
+class Compass:
+    """compass<LOSSFUNC, PARAM> (include/optimizer/compass.h:40-183), probes batched on the GPU.
+
+    Optimises model.parameter_values(flag) (default bsdf_attr::All: Dependent attributes are held
+    fixed) inside [lower, upper] (default: the model's parameter bounds); the model's parameters
+    are updated in place, like the reference's parameter references."""
+
+    def __init__(self, lossfunc, model=None, lower=None, upper=None, tolerance=EPSILON, step_size=1.0,
+                 contraction=0.5, expansion=1.0, flag=ALL):
+        self.loss = lossfunc
+        self.model = model if model is not None else lossfunc.fitted
+        self.idx = self.model.parameter_indices(flag)
+        full_lo = self.model.parameter_lower_bound()
+        full_hi = self.model.parameter_upper_bound()
+        self.lower = (np.asarray(lower, _F32) if lower is not None else full_lo[self.idx]).astype(_F32)
+        self.upper = (np.asarray(upper, _F32) if upper is not None else full_hi[self.idx]).astype(_F32)
+        self.directions = []
+        for i in range(1, len(self.idx) + 1):       # for(Scalar i=1; i <= size(param); ++i) (compass.h:67-71)
+            self.directions += [float(i), -float(i)]
+        self.initial_step = _F32(step_size)
+        self.tolerance = _F32(tolerance)
+        self.contraction, self.expansion = _F32(contraction), _F32(expansion)
+        self.reset()
+
+    def reset(self):
+        """compass.h:145-150: step size back to the initial one, loss of the current parameters."""
+        self.step_size = self.initial_step
+        self.loss_value = _F32(self.loss(self.model._params))
+
+    def is_converged(self):
+        return bool(self.step_size < self.tolerance)
+
+    def _params(self):
+        return self.model._params[self.idx].astype(_F32)
+
+    def step(self):
+        """One compass step (compass.h:82-140).  Returns the loss after the update."""
+        if self.is_converged():
+            return _F32(0)
+        param = self._params()
+        s = self.step_size
+        probes, in_box = [], []
+        full = self.model._params.copy()
+        for card in self.directions:
+            k = int(abs(card)) - 1
+            # probe(cardinal): value = param[k] + (cardinal < 0 ? -step : step), float arithmetic
+            param[k] = _F32(param[k] + (-s if card < 0 else s))
+            inb = bool(np.all((param >= self.lower) & (param <= self.upper)))
+            full[self.idx] = param
+            probes.append(full.copy())
+            in_box.append(inb)
+            # probe(-cardinal): the reference restores by the opposite update (not by assignment)
+            param[k] = _F32(param[k] + (s if card < 0 else -s))
+        probes = np.stack(probes)
+        in_box = np.asarray(in_box)
+        errs = np.zeros(len(probes), _F32)
+        if in_box.any():
+            errs[in_box] = self.loss.probe_losses(probes[in_box])
+        # sequential selection of the strictly best in-box probe (compass.h:118-121)
+        best, loss = 0.0, self.loss_value
+        for card, inb, err in zip(self.directions, in_box, errs):
+            if inb and err < loss:
+                best, loss = card, err
+        optimize = bool(loss < self.loss_value)
+        if optimize and best != 0:
+            k = int(abs(best)) - 1
+            param[k] = _F32(param[k] + (-s if best < 0 else s))
+        # the parameters keep any round-off of the probe/restore sequence, as the reference's do
+        self.model._params[self.idx] = param
+        self.step_size = _F32(self.expansion * s) if optimize else _F32(self.contraction * s)
+        if optimize:
+            self.loss_value = _F32(loss)
+        return self.loss_value

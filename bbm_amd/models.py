@@ -53,6 +53,17 @@ ATTRIBUTES = {
 }
 
 
+# Aggregate(Lambertian, X) registry keys -> children (aggregatemodel.h:22-233; the published fits'
+# form, fits/*.fit).  Parameters are the children's vectors concatenated in order.
+AGGREGATES = {f"Aggregate<Lambertian,{x}>": ("Lambertian", x) for x in (
+    "Bagher", "CookTorrance", "GGX", "LowCookTorrance", "LowAshikhminShirley", "LowMicrofacetFit", "LowSmooth",
+    "NganAshikhminShirley", "NganBlinnPhong", "NganCookTorrance", "NganLafortune", "NganWard", "NganWardDuer")}
+
+
+def aggregate_key(children):
+    return "Aggregate<" + ",".join(children) + ">"
+
+
 def attr_size(shape):
     n = 1
     for d in shape:
@@ -61,6 +72,8 @@ def attr_size(shape):
 
 
 def nparams(name):
+    if name in AGGREGATES:
+        return sum(nparams(c) for c in AGGREGATES[name])
     return sum(attr_size(s) for _, s in ATTRIBUTES[name])
 
 
@@ -79,7 +92,15 @@ def fmt_attr(values, shape):
 
 
 def to_string(name, params):
-    """bbm::toString(model): `Name(attr = value, ...)` in attribute declaration order."""
+    """bbm::toString(model): `Name(attr = value, ...)` in attribute declaration order;
+    aggregates print `Aggregate(child, child)` (aggregatemodel.h:168-179)."""
+    if name in AGGREGATES:
+        parts, k = [], 0
+        for c in AGGREGATES[name]:
+            n = nparams(c)
+            parts.append(to_string(c, params[k:k + n]))
+            k += n
+        return "Aggregate(" + ", ".join(parts) + ")"
     parts, k = [], 0
     for attr, shape in ATTRIBUTES[name]:
         n = attr_size(shape)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 1
+#define BBM_HIP_ABI_VERSION 2
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -71,6 +71,11 @@ int bbm_hip_model_nparams(int model_id);                /* length of the paramet
 int bbm_hip_model_params(int model_id, int which, float* out, int capacity);
 /* Component flags the model can return non-zero values for (BBM_FLAG_*). */
 int bbm_hip_model_components(int model_id);
+/* Per-parameter bsdf_attr flags (include/bbm/bsdf_attr_flag.h:16-29: DiffuseScale 0x01,
+ * DiffuseParameter 0x02, SpecularScale 0x04, SpecularParameter 0x08, Dependent 0x10), i.e. which
+ * entries bbm::parameter_values(model, flag) selects (include/bbm/bsdf_enumerate.h:103-131; the
+ * default flag All = 0x0F leaves out Dependent attributes).  Returns nparams. */
+int bbm_hip_model_param_attrs(int model_id, uint32_t* out, int capacity);
 
 /* ---------------------------------------------------------------- batched evaluation */
 
@@ -104,6 +109,66 @@ int bbm_hip_sample(int model_id, const float* params, int nparams,
                    const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
                    float* dir_x, float* dir_y, float* dir_z, float* pdf, uint32_t* flag,
                    void* stream);
+
+/* reflectance (RGB) for n outgoing directions -- bsdfmodel::reflectance, the (approximate)
+ * hemispherical reflectance, e.g. bsdfmodel/microfacet.h:182-196, lambertian.h:136-140; the
+ * weights aggregatemodel uses to mix its children's pdfs (aggregatemodel.h:81-150). */
+int bbm_hip_reflectance(int model_id, const float* params, int nparams,
+                        const float* out_x, const float* out_y, const float* out_z,
+                        const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                        float* r, float* g, float* b, void* stream);
+
+/* ---------------------------------------------------------------- fitting (BASELINE config 5) */
+
+/* Linearizer: a bijection between an index range [0, size) and (in, out) direction pairs
+ * (concepts/inout_linearizer.h).  kind BBM_LIN_SPHERICAL = spherical_linearizer
+ * (include/linearizer/spherical_linearizer.h:25-111): (phi, theta) grids of samples_in / samples_out
+ * points over [start, end] (theta end points included); kind BBM_LIN_MERL = merl_linearizer
+ * (include/linearizer/merl_linearizer.h:21-131): samples_in = samplesH (1, 90), samples_out =
+ * samplesD (180, 90) in (phi, theta) order -- theta_h quadratic, theta_d / phi_d linear, start/end
+ * unused. */
+#define BBM_LIN_SPHERICAL 0
+#define BBM_LIN_MERL 1
+typedef struct bbm_hip_linearizer
+{
+  int32_t kind;
+  uint64_t samples_in[2];
+  uint64_t samples_out[2];
+  float start_in[2], end_in[2], start_out[2], end_out[2];   /* (phi, theta), radians */
+} bbm_hip_linearizer;
+
+/* Number of direction pairs of the linearizer (linearizer::size()). */
+int bbm_hip_linearizer_size(const bbm_hip_linearizer* lin, uint64_t* size);
+
+/* Direction pairs begin .. begin + n - 1 of the linearizer into device SoA arrays. */
+int bbm_hip_linearize(const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
+                      float* in_x, float* in_y, float* in_z, float* out_x, float* out_y, float* out_z,
+                      void* stream);
+
+/* Sample losses (include/loss/cosine_weighted_l2.h, include/loss/cosine_weighted_log.h) */
+#define BBM_LOSS_NGAN_L2 0
+#define BBM_LOSS_LOW_L2 1
+#define BBM_LOSS_BIERON_L2 2
+#define BBM_LOSS_STANDARD_LOG 3
+#define BBM_LOSS_LOW_LOG 4
+#define BBM_LOSS_BIERON_LOG 5
+
+/* Workspace (bytes, device memory) bbm_hip_loss needs for nprobes probes. */
+size_t bbm_hip_loss_workspace_size(int nprobes);
+
+/* Multi-probe sampled loss -- sampledlossfunction::operator()() (include/bbm/sampledlossfunction.h:62-87)
+ * for nprobes parameter vectors at once (a compass step's 2P probes, include/optimizer/compass.h:82-140),
+ * over the samples begin .. begin + n - 1 of the linearizer (one GPU's shard):
+ *   sums[p] = sum_i loss(in_i, out_i, model(probes[p]).eval(in_i, out_i, component, unit), ref_i)
+ * accumulated in double; the caller divides by the linearizer size after summing the shards
+ * (RCCL all-reduce).  probes: device, nprobes x nparams floats; ref_r/g/b: device, the reference
+ * value of sample begin + i at [i]; sums: device, nprobes doubles; workspace: device,
+ * bbm_hip_loss_workspace_size(nprobes) bytes.  Deterministic (fixed reduction order). */
+int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
+                 const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
+                 const float* ref_r, const float* ref_g, const float* ref_b,
+                 int loss_kind, uint32_t component, uint32_t unit,
+                 double* sums, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- synthetic directions */
 

@@ -46,6 +46,62 @@ FITS = {
 }
 
 
+FIT_FILES = {   # Aggregate(Lambertian, X) -> the published fit used as the 'fit' parameter set (first entry)
+    "Aggregate<Lambertian,Bagher>": "bagher_sgd.fit",
+    "Aggregate<Lambertian,CookTorrance>": "low_cooktorrance_E1.fit",
+    "Aggregate<Lambertian,LowCookTorrance>": "low_cooktorrance_E1.fit",
+    "Aggregate<Lambertian,LowAshikhminShirley>": "low_ashikhminshirley_E1.fit",
+    "Aggregate<Lambertian,LowMicrofacetFit>": "low_lowmicrofacet_E2.fit",
+    "Aggregate<Lambertian,LowSmooth>": "low_lowsmooth_E2.fit",
+    "Aggregate<Lambertian,NganAshikhminShirley>": "ngan_ashikhminshirley.fit",
+    "Aggregate<Lambertian,NganBlinnPhong>": "ngan_blinnphong.fit",
+    "Aggregate<Lambertian,NganCookTorrance>": "ngan_cooktorrance.fit",
+    "Aggregate<Lambertian,NganLafortune>": "ngan_lafortune.fit",
+    "Aggregate<Lambertian,NganWard>": "ngan_ward.fit",
+    "Aggregate<Lambertian,NganWardDuer>": "ngan_wardduer.fit",
+}
+
+
+def fit_params(name):
+    """Parameter vector of the first material of the model's published fit file (fits/*.fit, `name =
+    Aggregate(...)`), parsed with the host mirror's fromString (attribute layout of bbm_amd/models.py)."""
+    sys.path.insert(0, ROOT)
+    from bbm_amd import models as bm
+    from bbm_amd.backbone import _parse_value, _tokenize
+    path = os.path.join("/root/reference/fits", FIT_FILES[name])
+    line = next(l for l in open(path) if "=" in l and not l.lstrip().startswith("#"))
+    tok = _tokenize(line.split("=", 1)[1])
+    # Aggregate ( Child ( attr = v , ... ) , Child ( ... ) )
+    out, i = [], 2
+    for child in bm.AGGREGATES[name]:
+        layout = bm.ATTRIBUTES[child]
+        vals = {}
+        i += 2
+        while tok[i] != ")":
+            attr = tok[i]
+            v, i = _parse_value(tok, i + 2)
+            vals[attr] = np.asarray(v, np.float32).reshape(-1)
+            if tok[i] == ",":
+                i += 1
+        i += 1
+        if tok[i] == ",":
+            i += 1
+        return_vals = []
+        for attr, shape in layout:
+            n = bm.attr_size(shape)
+            v = vals.get(attr)
+            if v is None:
+                return None          # attribute missing from the file: no 'fit' set
+            return_vals.append(np.repeat(v, n) if v.size == 1 and n > 1 else v)
+        out.append(np.concatenate(return_vals))
+    return np.concatenate(out).astype(np.float32)
+
+
+def golden_file(name):
+    """tests/golden file of a model: Aggregate<Lambertian,X> -> Aggregate_Lambertian_X.npz"""
+    return name.replace("<", "_").replace(",", "_").replace(">", "") + ".npz"
+
+
 def load_ref():
     path = os.path.join(HERE, "_ref", "libbbm_ref.so")
     if not os.path.exists(path):
@@ -133,6 +189,10 @@ def param_sets(name, defaults, lo, hi, rng):
     sets = [("default", np.asarray(defaults, np.float32))]
     if name in FITS:
         sets.append(("fit", np.asarray(FITS[name], np.float32)))
+    elif name in FIT_FILES:
+        fp = fit_params(name)
+        if fp is not None:
+            sets.append(("fit", fp))
     for k in range(2):
         p = []
         for d, a, b in zip(defaults, lo, hi):
@@ -187,6 +247,10 @@ def main():
                               fptr(so[0]), fptr(so[1]), fptr(so[2]), fptr(so[3]), fptr(sf), 1)
             arrays[f"sample{si}"] = so
             arrays[f"sflag{si}"] = sf.astype(np.uint8)
+            rf = np.zeros((3, M), np.float32)
+            lib.bbmref_reflectance(bname, fptr(p), k, ctypes.c_size_t(M), fptr(sout[0]), fptr(sout[1]), fptr(sout[2]),
+                                   FLAG_ALL, UNIT_RADIANCE, fptr(rf[0]), fptr(rf[1]), fptr(rf[2]))
+            arrays[f"reflectance{si}"] = rf
         p = sets[0][1]
         for tag, comp, unit in (("diffuse", FLAG_DIFFUSE, UNIT_RADIANCE), ("specular", FLAG_SPECULAR, UNIT_RADIANCE),
                                 ("importance", FLAG_ALL, UNIT_IMPORTANCE)):
@@ -204,9 +268,17 @@ def main():
         lib.bbmref_reflectance(bname, fptr(p), k, ctypes.c_size_t(M), fptr(sout[0]), fptr(sout[1]), fptr(sout[2]),
                                FLAG_ALL, UNIT_RADIANCE, fptr(rf[0]), fptr(rf[1]), fptr(rf[2]))
         arrays["reflectance"] = rf
-        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrays)
+        for tag, comp in (("diffuse", FLAG_DIFFUSE), ("specular", FLAG_SPECULAR)):
+            rf = np.zeros((3, M), np.float32)
+            lib.bbmref_reflectance(bname, fptr(p), k, ctypes.c_size_t(M), fptr(sout[0]), fptr(sout[1]), fptr(sout[2]),
+                                   comp, UNIT_RADIANCE, fptr(rf[0]), fptr(rf[1]), fptr(rf[2]))
+            arrays[f"reflectance_{tag}"] = rf
+        abuf = (ctypes.c_uint32 * 64)()
+        ka = lib.bbmref_param_attrs(bname, abuf, 64)
+        attrs = [int(abuf[j]) for j in range(ka)]
+        np.savez_compressed(os.path.join(OUT, golden_file(name)), **arrays)
         meta["models"][name] = {"nparams": k, "defaults": defaults, "lower": lo, "upper": hi,
-                                "sets": [t for t, _ in sets], "strings": strings}
+                                "sets": [t for t, _ in sets], "strings": strings, "attrs": attrs}
         print(f"{name:24s} k={k:2d} sets={len(sets)}")
     with open(os.path.join(OUT, "models.json"), "w") as f:
         json.dump(meta, f, indent=1)

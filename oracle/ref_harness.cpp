@@ -19,179 +19,15 @@
  * default NTTP name fails CTAD on g++ 11, include/ndf/sampler.h:34), EPD (needs the missing
  * precomputed/holzschuchpacanowski/{convolution,normalization}.h blobs), Merl (needs MERL data).
  */
-#include "bbm/bbm_core.h"
-#include "bbm/bsdf_enumerate.h"
-#include "bsdfmodel/scaledmodel.h"
-#include "bsdfmodel/microfacet.h"
-#include "bsdfmodel/aggregatemodel.h"
-#include "bsdfmodel/lambertian.h"
-#include "bsdfmodel/orennayar.h"
-#include "bsdfmodel/cooktorrance.h"
-#include "bsdfmodel/cooktorranceheitz.h"
-#include "bsdfmodel/cooktorrancewalter.h"
-#include "bsdfmodel/ggx.h"
-#include "bsdfmodel/ggxheitz.h"
-#include "bsdfmodel/phongwalter.h"
-#include "bsdfmodel/ribardiere.h"
-#include "bsdfmodel/bagher.h"
-#include "bsdfmodel/lowmicrofacet.h"
-#include "bsdfmodel/ward.h"
-#include "bsdfmodel/wardduer.h"
-#include "bsdfmodel/wardduergeislermoroder.h"
-#include "bsdfmodel/phong.h"
-#include "bsdfmodel/lafortune.h"
-#include "bsdfmodel/ashikhminshirley.h"
-#include "bsdfmodel/ashikhminshirleyfull.h"
-#include "bsdfmodel/lowsmooth.h"
-#include "bsdfmodel/he.h"
-#include "bsdfmodel/low.h"
-// ngan.h:169 concept-checks NganHe, whose ndf_sampler default NAME fails CTAD on g++ 11
-// (include/ndf/sampler.h:34).  The check is a compile-time static_assert only; it is switched
-// off for this one header so the six other Ngan models (which do compile) can be instantiated.
-#pragma push_macro("BBM_CHECK_CONCEPT")
-#undef BBM_CHECK_CONCEPT
-#define BBM_CHECK_CONCEPT(...) static_assert(true, "")
-#include "bsdfmodel/ngan.h"
-#pragma pop_macro("BBM_CHECK_CONCEPT")
+#include "ref_ops.hpp"
 
-#include <cstdint>
-#include <cstring>
-#include <sstream>
-#include <string>
-#include <vector>
-#ifdef _OPENMP
-#include <omp.h>
-#endif
+namespace bbmref {
+// aggregates of two models, defined in ref_fit.cpp
+const std::vector<entry>& aggregate_registry();
+}
 
 namespace {
-
-constexpr bbm::bsdf_attr kAllParams = bbm::bsdf_attr(0x1F);   // All | Dependent
-
-template<typename M>
-struct ops
-{
-  using Value = typename M::Value;
-  using Vec3d = typename M::Vec3d;
-  using Vec2d = typename M::Vec2d;
-
-  static std::vector<float> defaults()
-  {
-    M m;
-    std::vector<float> r;
-    for(auto& v : bbm::parameter_values(m, kAllParams)) r.push_back(float(v));
-    return r;
-  }
-
-  static M make(const float* p, int np)
-  {
-    M m;
-    auto pv = bbm::parameter_values(m, kAllParams);
-    for(size_t i = 0; i < pv.size() && int(i) < np; ++i) pv[i] = Value(p[i]);
-    return m;
-  }
-
-  static std::vector<float> bounds(bool upper)
-  {
-    M m;
-    std::vector<float> r;
-    auto b = upper ? bbm::parameter_upper_bound(m, kAllParams) : bbm::parameter_lower_bound(m, kAllParams);
-    for(auto& v : b) r.push_back(float(v));
-    return r;
-  }
-
-  static std::string to_string(const float* p, int np)
-  {
-    M m = make(p, np);
-    std::ostringstream s;
-    s << bbm::toString(m);
-    return s.str();
-  }
-
-  // mode bit 1 = eval, bit 2 = pdf
-  template<typename OUT>
-  static void evalpdf(const float* p, int np, size_t n,
-                      const float* ix, const float* iy, const float* iz,
-                      const float* ox, const float* oy, const float* oz,
-                      uint32_t component, uint32_t unit, int mode,
-                      OUT* r, OUT* g, OUT* b, OUT* pdf, int nthreads)
-  {
-    const M m = make(p, np);
-    const auto comp = bbm::bsdf_flag(component);
-    const auto u = bbm::unit_t(unit);
-#ifdef _OPENMP
-    #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
-#endif
-    for(size_t i = 0; i < n; ++i)
-    {
-      Vec3d in(Value(ix[i]), Value(iy[i]), Value(iz[i]));
-      Vec3d out(Value(ox[i]), Value(oy[i]), Value(oz[i]));
-      if(mode & 1)
-      {
-        auto e = m.eval(in, out, comp, u);
-        r[i] = OUT(e[0]); g[i] = OUT(e[1]); b[i] = OUT(e[2]);
-      }
-      if(mode & 2) pdf[i] = OUT(m.pdf(in, out, comp, u));
-    }
-  }
-
-  template<typename OUT>
-  static void sample(const float* p, int np, size_t n,
-                     const float* ox, const float* oy, const float* oz,
-                     const float* xi0, const float* xi1,
-                     uint32_t component, uint32_t unit,
-                     OUT* dx, OUT* dy, OUT* dz, OUT* pdf, uint32_t* flag, int nthreads)
-  {
-    const M m = make(p, np);
-    const auto comp = bbm::bsdf_flag(component);
-    const auto u = bbm::unit_t(unit);
-#ifdef _OPENMP
-    #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
-#endif
-    for(size_t i = 0; i < n; ++i)
-    {
-      Vec3d out(Value(ox[i]), Value(oy[i]), Value(oz[i]));
-      Vec2d xi(Value(xi0[i]), Value(xi1[i]));
-      auto s = m.sample(out, xi, comp, u);
-      dx[i] = OUT(s.direction[0]); dy[i] = OUT(s.direction[1]); dz[i] = OUT(s.direction[2]);
-      pdf[i] = OUT(s.pdf);
-      flag[i] = uint32_t(s.flag);
-    }
-  }
-
-  static void reflectance(const float* p, int np, size_t n, const float* ox, const float* oy, const float* oz,
-                          uint32_t component, uint32_t unit, float* r, float* g, float* b)
-  {
-    const M m = make(p, np);
-    for(size_t i = 0; i < n; ++i)
-    {
-      Vec3d out(Value(ox[i]), Value(oy[i]), Value(oz[i]));
-      auto e = m.reflectance(out, bbm::bsdf_flag(component), bbm::unit_t(unit));
-      r[i] = float(e[0]); g[i] = float(e[1]); b[i] = float(e[2]);
-    }
-  }
-};
-
-struct entry
-{
-  const char* name;
-  std::vector<float> (*defaults)();
-  std::vector<float> (*bounds)(bool);
-  std::string (*to_string)(const float*, int);
-  void (*evalpdf_f)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, int, float*, float*, float*, float*, int);
-  void (*evalpdf_d)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, int, double*, double*, double*, double*, int);
-  void (*sample_f)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*, float*, uint32_t*, int);
-  void (*reflectance_f)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*);
-};
-
-#define BBMREF_ENTRY(MODEL) \
-  entry{ bbm::MODEL<bbm::floatRGB>::name.value, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::defaults, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::bounds, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::to_string, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::template evalpdf<float>, \
-         &ops<bbm::MODEL<bbm::doubleRGB>>::template evalpdf<double>, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::template sample<float>, \
-         &ops<bbm::MODEL<bbm::floatRGB>>::reflectance }
+using namespace bbmref;
 
 const std::vector<entry>& registry()
 {
@@ -232,6 +68,7 @@ const std::vector<entry>& registry()
 const entry* find(const char* name)
 {
   for(auto& e : registry()) if(std::strcmp(e.name, name) == 0) return &e;
+  for(auto& e : aggregate_registry()) if(std::strcmp(e.name, name) == 0) return &e;
   return nullptr;
 }
 
@@ -245,8 +82,15 @@ int copy_vec(const std::vector<float>& v, float* out, int cap)
 
 extern "C" {
 
-int bbmref_num_models(void) { return int(registry().size()); }
-const char* bbmref_model_name(int i) { return (i >= 0 && i < int(registry().size())) ? registry()[i].name : nullptr; }
+// single models first, then the Aggregate(Lambertian, X) entries of ref_fit.cpp
+int bbmref_num_models(void) { return int(registry().size() + aggregate_registry().size()); }
+const char* bbmref_model_name(int i)
+{
+  const int a = int(registry().size()), b = int(aggregate_registry().size());
+  if(i >= 0 && i < a) return registry()[size_t(i)].name;
+  if(i >= a && i < a + b) return aggregate_registry()[size_t(i - a)].name;
+  return nullptr;
+}
 
 int bbmref_default_params(const char* name, float* out, int cap)
 { auto e = find(name); return e ? copy_vec(e->defaults(), out, cap) : -1; }

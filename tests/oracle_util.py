@@ -133,7 +133,7 @@ def golden_inputs():
 
 
 def golden_model(name):
-    return np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    return np.load(os.path.join(GOLDEN, name.replace("<", "_").replace(",", "_").replace(">", "") + ".npz"))
 
 
 # ------------------------------------------------------------------------------ comparison
@@ -201,3 +201,84 @@ def dirgen_numpy(seed, stream_id, offset, n, mode=0):
     s = np.sqrt(np.maximum(1.0 - z * z, 0.0))
     phi = 2.0 * np.pi * u2
     return np.stack([s * np.cos(phi), s * np.sin(phi), z]).astype(np.float32)
+
+
+# ------------------------------------------------------------------------------ fitting
+
+def golden_fit():
+    with open(os.path.join(GOLDEN, "fit.json")) as f:
+        meta = json.load(f)
+    return meta, np.load(os.path.join(GOLDEN, "fit.npz"))
+
+
+def _grid_desc(g):
+    s_in = np.asarray(g["samples_in"], np.uint64)
+    s_out = np.asarray(g["samples_out"], np.uint64)
+    rng = np.asarray(list(g["start_in"]) + list(g["end_in"]) + list(g["start_out"]) + list(g["end_out"]), np.float32)
+    return s_in, s_out, rng
+
+
+def ref_loss_total(name, fitted, reference, grid, loss_kind):
+    """The reference's own sampledlossfunction()() total (serial float sum / N) on a spherical grid."""
+    lib = ref()
+    s_in, s_out, rng = _grid_desc(grid)
+    fitted = np.ascontiguousarray(fitted, np.float32)
+    reference = np.ascontiguousarray(reference, np.float32)
+    tot = np.zeros(1, np.float32)
+    n = lib.bbmref_loss(name.encode(), _fp(fitted), _fp(reference), fitted.size, 0, _fp(s_in), _fp(s_out), _fp(rng),
+                        loss_kind, None, _fp(tot), 1)
+    assert n > 0
+    return np.float32(tot[0])
+
+
+def ref_pair_losses(name, fitted, reference, din, dout, loss_kind, nthreads=8):
+    """Per-sample reference losses on explicit direction pairs (the reference's sampledlossfunction
+    over a table linearizer, oracle/ref_fit.cpp): (n,) float32."""
+    lib = ref()
+    din = np.ascontiguousarray(din, np.float32)
+    dout = np.ascontiguousarray(dout, np.float32)
+    n = din.shape[1]
+    ptrs = (ctypes.c_void_p * 6)(*[din[k].ctypes.data for k in range(3)] + [dout[k].ctypes.data for k in range(3)])
+    s_in = np.asarray([n, 0], np.uint64)
+    fitted = np.ascontiguousarray(fitted, np.float32)
+    reference = np.ascontiguousarray(reference, np.float32)
+    per = np.zeros(n, np.float32)
+    rc = lib.bbmref_loss(name.encode(), _fp(fitted), _fp(reference), fitted.size, 2, _fp(s_in), _fp(s_in),
+                         ctypes.cast(ptrs, ctypes.c_void_p), loss_kind, _fp(per), None, nthreads)
+    assert rc == n, rc
+    return per
+
+
+def ref_merl_index(din, dout, h=(1, 90), d=(180, 90)):
+    """The reference merl_linearizer's inverse map (direction pair -> index)."""
+    lib = ref()
+    din = np.ascontiguousarray(din, np.float32)
+    dout = np.ascontiguousarray(dout, np.float32)
+    n = din.shape[1]
+    idx = np.zeros(n, np.uint64)
+    sh = np.asarray(h, np.uint64)
+    sd = np.asarray(d, np.uint64)
+    lib.bbmref_merl_index(_fp(sh), _fp(sd), ctypes.c_size_t(n), _fp(din[0]), _fp(din[1]), _fp(din[2]), _fp(dout[0]),
+                          _fp(dout[1]), _fp(dout[2]), _fp(idx))
+    return idx
+
+
+class RefTotalLoss:
+    """A SampledLoss stand-in scored by the reference itself (serial float totals): drives the host
+    compass logic of bbm_amd.fit.Compass on the CPU with exactly the reference's loss values."""
+
+    def __init__(self, fitted, reference_params, grid, loss_kind):
+        self.fitted = fitted
+        self.reference = np.asarray(reference_params, np.float32)
+        self.grid = grid
+        self.loss_kind = loss_kind
+        self.calls = 0
+
+    def probe_losses(self, probes):
+        self.calls += 1
+        return np.array([ref_loss_total(self.fitted.name, p, self.reference, self.grid, self.loss_kind)
+                         for p in np.asarray(probes, np.float32)], np.float32)
+
+    def __call__(self, params=None):
+        p = self.fitted._params if params is None else params
+        return float(self.probe_losses(np.asarray(p, np.float32)[None])[0])

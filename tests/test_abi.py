@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 1
+    assert lib.bbm_hip_abi_version() == 2
 
 
 def test_registry_matches_reference(lib):
@@ -63,10 +63,53 @@ def test_registry_matches_reference(lib):
 
 
 def test_python_mirror_layout_covers_every_reference_model():
-    from bbm_amd.models import ATTRIBUTES, nparams
+    from bbm_amd.models import AGGREGATES, ATTRIBUTES, nparams
     for name, ref in META["models"].items():
-        assert name in ATTRIBUTES, name
+        assert name in ATTRIBUTES or name in AGGREGATES, name
         assert nparams(name) == ref["nparams"], name
+
+
+def test_param_attrs_match_reference(lib):
+    """bsdf_attr flags per parameter == what bbm::parameter_values(model, flag) selects in the reference."""
+    names = [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
+    assert set(names) == set(META["models"])
+    for i, name in enumerate(names):
+        ref = META["models"][name]["attrs"]
+        buf = (ctypes.c_uint32 * 64)()
+        assert lib.bbm_hip_model_param_attrs(i, buf, 64) == len(ref)
+        assert [int(buf[j]) for j in range(len(ref))] == ref, name
+
+
+def test_fit_abi_validation(lib):
+    from bbm_amd import _lib, fit
+    lin = fit.spherical_linearizer((8, 5), (6, 4))
+    assert lin.size() == 8 * 5 * 6 * 4
+    assert fit.merl_linearizer().size() == 90 * 90 * 180
+    bad = fit.spherical_linearizer((0, 5), (6, 4))
+    n = ctypes.c_uint64()
+    assert lib.bbm_hip_linearizer_size(ctypes.byref(bad), ctypes.byref(n)) == _lib.ERR_INVALID_ARG
+    assert lib.bbm_hip_loss_workspace_size(36) >= 36 * 8
+    agg = lib.bbm_hip_model_id(b"Aggregate<Lambertian,Bagher>")
+    assert agg >= 0 and lib.bbm_hip_model_nparams(agg) == 33
+    # wrong parameter count, unknown loss, missing workspace: rejected before any launch
+    assert lib.bbm_hip_loss(agg, None, 30, 4, ctypes.byref(lin), 0, 16, None, None, None, 3, 3, 0, None, None, 0,
+                            None) == _lib.ERR_INVALID_ARG
+    assert lib.bbm_hip_loss(agg, None, 33, 4, ctypes.byref(lin), 0, 16, None, None, None, 9, 3, 0, None, None, 0,
+                            None) == _lib.ERR_INVALID_ARG
+    assert lib.bbm_hip_loss(agg, None, 33, 4, ctypes.byref(lin), 0, lin.size() + 1, None, None, None, 3, 3, 0, None,
+                            None, 0, None) == _lib.ERR_INVALID_ARG
+    assert b"out of bounds" in lib.bbm_hip_last_error()
+
+
+def test_aggregate_mirror():
+    import bbm_amd
+    fitted = bbm_amd.Aggregate(bbm_amd.Lambertian(), bbm_amd.Bagher())
+    assert fitted.name == "Aggregate<Lambertian,Bagher>"
+    # bsdf_attr::All selects the 18 non-Dependent parameters (compass's P, SURVEY.md a13)
+    assert len(fitted.parameter_indices()) == 18
+    assert [c.name for c in fitted.children()] == ["Lambertian", "Bagher"]
+    s = META["models"]["Aggregate<Lambertian,Bagher>"]["strings"][1]
+    assert str(bbm_amd.fromString(s)) == s
 
 
 @pytest.mark.parametrize("name", sorted(META["models"]))
