@@ -220,10 +220,15 @@ struct Lafortune
   {
     const bool m = component & kFlagSpecular;
     const v3 co = mk3(cx * out.x, cy * out.y, cz * out.z);
-    const float nrm = powf(sqrtf(dot3(co, co)), s) * kPi2F;
+    const float nrm = powf_cr(sqrtf(dot3(co, co)), s) * kPi2F;
     const float normalization = div_nr(nrm, s + 2);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] * normalization : 0.0f;
+    for (int c = 0; c < 3; ++c)
+    {
+      float v = albedo[c] * normalization;
+      if (NGAN) v = float(double(v) * ngan);      // ngan.h:123: result *= Ngan normalization (double)
+      rgb[c] = m ? v : 0.0f;
+    }
   }
 
   __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
@@ -502,8 +507,8 @@ struct LowSmooth
   __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
   {
     const bool m = (component & kFlagSpecular) && (out.z > 0);
-    const float f1 = div_nr(logf(B + 1), 2 * B);
-    const float f2 = float((1.0 - double(powf(B + 1, 1 - C))) / double(2 * B * (C - 1)));
+    const float f1 = div_nr(logf_cr(B + 1), 2 * B);
+    const float f2 = float((1.0 - double(powf_cr(B + 1, 1 - C))) / double(2 * B * (C - 1)));
     const float factor = (fabsf(C - 1) < kEpsF) ? f1 : f2;
     const float q = div_nr(fres.eta - 1, fres.eta + 1);
     const float R0 = q * q;

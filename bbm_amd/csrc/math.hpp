@@ -185,5 +185,7 @@ __device__ __forceinline__ float pow2f(float x) { return x * x; }
 // 1-ulp expf difference is not amplified; the eval kernels keep the full-rate f32 expf.
 __device__ __forceinline__ float expf_cr(float x) { return float(exp(double(x))); }
 __device__ __forceinline__ float logf_cr(float x) { return float(log(double(x))); }
+// glibc powf (what std::pow(float, float) calls) is computed in double and rounded once; so is this
+__device__ __forceinline__ float powf_cr(float x, float y) { return float(pow(double(x), double(y))); }
 
 }  // namespace bbmhip

@@ -282,3 +282,28 @@ class RefTotalLoss:
     def __call__(self, params=None):
         p = self.fitted._params if params is None else params
         return float(self.probe_losses(np.asarray(p, np.float32)[None])[0])
+
+
+def merl_directions_f64(h=(1, 90), d=(180, 90)):
+    """merl_linearizer's index -> direction map (include/linearizer/merl_linearizer.h:49-83) evaluated in
+    float64 (numpy): the sample at index i sits on the lower edge of its (theta_h, theta_d, phi_d) bin;
+    convertFromHalfwayDifference (include/core/vec_transform.h:118-123) = rotZ(phi_h) rotY(theta_h)."""
+    n = d[0] * d[1] * h[1]
+    i = np.arange(n, dtype=np.int64)
+    pd = i % d[0]
+    td = (i // d[0]) % d[1]
+    th = i // (d[0] * d[1])
+    theta_h = (th / h[1]) ** 2 * (0.5 * np.pi)
+    phi_d = pd / d[0] * np.pi
+    theta_d = td / d[1] * (0.5 * np.pi)
+    diff = np.stack([np.cos(phi_d) * np.sin(theta_d), np.sin(phi_d) * np.sin(theta_d), np.cos(theta_d)])
+    cy, sy = np.cos(theta_h), np.sin(theta_h)
+
+    def rot(v):      # phi_h == 0: rotZ is the identity
+        return np.stack([cy * v[0] + sy * v[2], v[1], -sy * v[0] + cy * v[2]])
+
+    din = rot(diff)
+    dout = rot(np.stack([-diff[0], -diff[1], diff[2]]))
+    din[2] = np.maximum(din[2], 0)
+    dout[2] = np.maximum(dout[2], 0)
+    return din, dout

@@ -56,21 +56,34 @@ def test_spherical_linearizer_matches_reference(bbm, gname):
 
 
 def test_merl_linearizer_round_trips_through_reference_inverse(bbm):
+    """The MERL grid (90 x 90 x 180): (1) GPU directions == the forward map evaluated in float64 within
+    float round-off; (2) the reference's inverse map sends them back to their own index.  Every MERL
+    sample sits exactly on the lower edge of its bin (idx / samples, merl_linearizer.h:74-75), so the
+    inverse's floor(x + Epsilon) (:116-117) flips to the bin below whenever float round-off of the
+    round trip exceeds Epsilon: the reference loses the same samples on the float64 directions rounded
+    to float, and a flip is never more than one bin."""
     from bbm_amd import fit
     lin = fit.merl_linearizer()
     n = lin.size()
     assert n == 90 * 90 * 180
     din, dout = lin.directions()
     din, dout = din.cpu().numpy(), dout.cpu().numpy()
-    idx = ou.ref_merl_index(din, dout)
-    want = np.arange(n, dtype=np.uint64)
-    td = (want // 180) % 90
-    th = want // (180 * 90)
+    rin, rout = ou.merl_directions_f64()
+    err = max(np.abs(din - rin).max(), np.abs(dout - rout).max())
+    assert err <= 2e-6, f"forward map off by {err}"
+    idx = ou.ref_merl_index(din, dout).astype(np.int64)
+    idx64 = ou.ref_merl_index(rin.astype(np.float32), rout.astype(np.float32)).astype(np.int64)
+    want = np.arange(n, dtype=np.int64)
+    td, th = (want // 180) % 90, want // (180 * 90)
     # well-posed samples: phi_d defined (theta_d > 0) and both directions strictly above the horizon
     ok = (td > 0) & (din[2] > 1e-3) & (dout[2] > 1e-3)
-    frac = np.mean(idx[ok] == want[ok])
-    bad = np.nonzero(ok & (idx != want))[0]
-    assert frac > 0.999, f"round trip {frac:.5f}; e.g. idx {want[bad[:5]]} -> {idx[bad[:5]]}"
+    frac, frac64 = np.mean(idx[ok] == want[ok]), np.mean(idx64[ok] == want[ok])
+    assert frac > 0.975 and frac >= frac64 - 0.005, f"round trip {frac:.5f} (float64 directions: {frac64:.5f})"
+    bad = ok & (idx != want)
+    dth = idx[bad] // (180 * 90) - th[bad]
+    dtd = (idx[bad] // 180) % 90 - td[bad]
+    dpd = (idx[bad] % 180 - want[bad] % 180 + 90) % 180 - 90          # phi_d is cyclic
+    assert np.all(np.abs(dth) <= 1) and np.all(np.abs(dtd) <= 1) and np.all(np.abs(dpd) <= 1)
     # theta_d == 0 (in == out): the inverse map sets phi_d = 0 (merl_linearizer.h:110-111)
     sel = (td == 0) & (din[2] > 1e-3)
     assert np.all(idx[sel] == (th[sel] * 90 * 180))

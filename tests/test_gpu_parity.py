@@ -131,6 +131,25 @@ def test_every_gpu_model_matches_reference_golden(bbm):
     _report("golden", worst)
 
 
+def test_reflectance_matches_reference_golden(bbm):
+    """reflectance(out) (concepts/bsdfmodel.h: Spectrum reflectance(out, component, unit, mask)) for
+    every parameter set and per component; it is also the sampling weight of Aggregate models."""
+    worst = {}
+    for name in _gpu_models(bbm):
+        g = ou.golden_model(name)
+        for si in range(len(META["models"][name]["sets"])):
+            m = bbm.BsdfModel(name)
+            m.set_parameter_values(g[f"params{si}"])
+            got = m.reflectance(_dev(INP["sout"])).cpu().numpy()
+            worst[f"{name}[{si}]"] = _assert_parity(got, g[f"reflectance{si}"], f"{name}[{si}] reflectance")
+        m = bbm.BsdfModel(name)
+        m.set_parameter_values(g["params0"])
+        for tag, comp in (("diffuse", 1), ("specular", 2)):
+            got = m.reflectance(_dev(INP["sout"]), component=bbm.bsdf_flag(comp)).cpu().numpy()
+            _assert_parity(got, g[f"reflectance_{tag}"], f"{name}/{tag} reflectance")
+    _report("reflectance", worst)
+
+
 @pytest.mark.parametrize("tag,comp,unit", [("diffuse", 1, 0), ("specular", 2, 0), ("importance", 3, 1)])
 def test_component_and_unit_semantics(bbm, tag, comp, unit):
     for name in _gpu_models(bbm):
