@@ -42,6 +42,7 @@ struct ModelEntry
   SampleLauncher sample;
   ReflLauncher reflectance;
   LossLauncher loss;
+  CheckLauncher check;
   float defaults[kMaxParams];
   float lower[kMaxParams];
   float upper[kMaxParams];
@@ -57,66 +58,66 @@ constexpr float kFMin = 1.1754943508222875e-38f;
 // reported by parameter_lower_bound/upper_bound, ior 1.3 in [1,5]); pinned against
 // tests/golden/models.json by tests/test_abi.py.
 const ModelEntry kSingle[] = {
-  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>, &launch_sample<Lambertian>, &launch_reflectance<Lambertian>, &launch_loss<Lambertian>,
+  {"Lambertian", 3, kFlagDiffuse, &launch_eval_pdf<Lambertian>, &launch_sample<Lambertian>, &launch_reflectance<Lambertian>, &launch_loss<Lambertian>, &launch_check<Lambertian>,
    {0.5f, 0.5f, 0.5f}, {0, 0, 0}, {1, 1, 1}, "ddd"},
-  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>,
+  {"CookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>, &launch_check<CookTorranceM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
-  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>,   // bsdfmodel/low.h:32-33
+  {"LowCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceM>, &launch_sample<CookTorranceM>, &launch_reflectance<CookTorranceM>, &launch_loss<CookTorranceM>, &launch_check<CookTorranceM>,   // bsdfmodel/low.h:32-33
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
-  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>, &launch_sample<GGXM>, &launch_reflectance<GGXM>, &launch_loss<GGXM>,
+  {"GGX", 5, kFlagSpecular, &launch_eval_pdf<GGXM>, &launch_sample<GGXM>, &launch_reflectance<GGXM>, &launch_loss<GGXM>, &launch_check<GGXM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
-  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>, &launch_reflectance<CookTorranceWalterM>, &launch_loss<CookTorranceWalterM>,
+  {"CookTorranceWalter", 5, kFlagSpecular, &launch_eval_pdf<CookTorranceWalterM>, &launch_sample<CookTorranceWalterM>, &launch_reflectance<CookTorranceWalterM>, &launch_loss<CookTorranceWalterM>, &launch_check<CookTorranceWalterM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, 1}, {1, 1, 1, 1, 5}, "ssspp"},
-  {"CookTorranceHeitz", 6, kFlagSpecular, &launch_eval_pdf<CookTorranceHeitzM>, &launch_sample<CookTorranceHeitzM>, &launch_reflectance<CookTorranceHeitzM>, &launch_loss<CookTorranceHeitzM>,
+  {"CookTorranceHeitz", 6, kFlagSpecular, &launch_eval_pdf<CookTorranceHeitzM>, &launch_sample<CookTorranceHeitzM>, &launch_reflectance<CookTorranceHeitzM>, &launch_loss<CookTorranceHeitzM>, &launch_check<CookTorranceHeitzM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}, "sssppp"},
-  {"GGXHeitz", 6, kFlagSpecular, &launch_eval_pdf<GGXHeitzM>, &launch_sample<GGXHeitzM>, &launch_reflectance<GGXHeitzM>, &launch_loss<GGXHeitzM>,
+  {"GGXHeitz", 6, kFlagSpecular, &launch_eval_pdf<GGXHeitzM>, &launch_sample<GGXHeitzM>, &launch_reflectance<GGXHeitzM>, &launch_loss<GGXHeitzM>, &launch_check<GGXHeitzM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1}, {1, 1, 1, 1, 1, 5}, "sssppp"},
-  {"NganCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<NganCookTorranceM>, &launch_sample<NganCookTorranceM>, &launch_reflectance<NganCookTorranceM>, &launch_loss<NganCookTorranceM>,
+  {"NganCookTorrance", 5, kFlagSpecular, &launch_eval_pdf<NganCookTorranceM>, &launch_sample<NganCookTorranceM>, &launch_reflectance<NganCookTorranceM>, &launch_loss<NganCookTorranceM>, &launch_check<NganCookTorranceM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, 0}, {1, 1, 1, 1, 1}, "ssspp"},
-  {"PhongWalter", 5, kFlagSpecular, &launch_eval_pdf<PhongWalterM>, &launch_sample<PhongWalterM>, &launch_reflectance<PhongWalterM>, &launch_loss<PhongWalterM>,
+  {"PhongWalter", 5, kFlagSpecular, &launch_eval_pdf<PhongWalterM>, &launch_sample<PhongWalterM>, &launch_reflectance<PhongWalterM>, &launch_loss<PhongWalterM>, &launch_check<PhongWalterM>,
    {0.5f, 0.5f, 0.5f, 32.0f, 1.3f}, {0, 0, 0, 0, 1}, {1, 1, 1, kFMax, 5}, "ssspp"},
-  {"Ribardiere", 6, kFlagSpecular, &launch_eval_pdf<RibardiereM>, &launch_sample<RibardiereM>, &launch_reflectance<RibardiereM>, &launch_loss<RibardiereM>,
+  {"Ribardiere", 6, kFlagSpecular, &launch_eval_pdf<RibardiereM>, &launch_sample<RibardiereM>, &launch_reflectance<RibardiereM>, &launch_loss<RibardiereM>, &launch_check<RibardiereM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 40, 5}, "sssppp"},
-  {"RibardiereAnisotropic", 7, kFlagSpecular, &launch_eval_pdf<RibardiereAnisoM>, &launch_sample<RibardiereAnisoM>, &launch_reflectance<RibardiereAnisoM>, &launch_loss<RibardiereAnisoM>,
+  {"RibardiereAnisotropic", 7, kFlagSpecular, &launch_eval_pdf<RibardiereAnisoM>, &launch_sample<RibardiereAnisoM>, &launch_reflectance<RibardiereAnisoM>, &launch_loss<RibardiereAnisoM>, &launch_check<RibardiereAnisoM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 2.0f, 1.3f}, {0, 0, 0, kEpsF, kEpsF, 1.5f + kEpsF, 1}, {1, 1, 1, 1, 1, 40, 5}, "ssspppp"},
-  {"OrenNayar", 4, kFlagDiffuse, &launch_eval_pdf<OrenNayar>, &launch_sample<OrenNayar>, &launch_reflectance<OrenNayar>, &launch_loss<OrenNayar>,
+  {"OrenNayar", 4, kFlagDiffuse, &launch_eval_pdf<OrenNayar>, &launch_sample<OrenNayar>, &launch_reflectance<OrenNayar>, &launch_loss<OrenNayar>, &launch_check<OrenNayar>,
    {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "dddD"},
-  {"LowMicrofacet", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>,
+  {"LowMicrofacet", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>, &launch_check<LowMicrofacetM>,
    {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
-  {"LowMicrofacetFit", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>,
+  {"LowMicrofacetFit", 6, kFlagSpecular, &launch_eval_pdf<LowMicrofacetM>, &launch_sample<LowMicrofacetM>, &launch_reflectance<LowMicrofacetM>, &launch_loss<LowMicrofacetM>, &launch_check<LowMicrofacetM>,
    {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
-  {"Ward", 5, kFlagSpecular, &launch_eval_pdf<WardM>, &launch_sample<WardM>, &launch_reflectance<WardM>, &launch_loss<WardM>,
+  {"Ward", 5, kFlagSpecular, &launch_eval_pdf<WardM>, &launch_sample<WardM>, &launch_reflectance<WardM>, &launch_loss<WardM>, &launch_check<WardM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
-  {"WardDuer", 5, kFlagSpecular, &launch_eval_pdf<WardDuerM>, &launch_sample<WardDuerM>, &launch_reflectance<WardDuerM>, &launch_loss<WardDuerM>,
+  {"WardDuer", 5, kFlagSpecular, &launch_eval_pdf<WardDuerM>, &launch_sample<WardDuerM>, &launch_reflectance<WardDuerM>, &launch_loss<WardDuerM>, &launch_check<WardDuerM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
-  {"WardDuerGeislerMoroder", 5, kFlagSpecular, &launch_eval_pdf<WardDGMM>, &launch_sample<WardDGMM>, &launch_reflectance<WardDGMM>, &launch_loss<WardDGMM>,
+  {"WardDuerGeislerMoroder", 5, kFlagSpecular, &launch_eval_pdf<WardDGMM>, &launch_sample<WardDGMM>, &launch_reflectance<WardDGMM>, &launch_loss<WardDGMM>, &launch_check<WardDGMM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f}, {0, 0, 0, kEpsF, kEpsF}, {1, 1, 1, 1, 1}, "ssspp"},
-  {"NganWard", 4, kFlagSpecular, &launch_eval_pdf<NganWardM>, &launch_sample<NganWardM>, &launch_reflectance<NganWardM>, &launch_loss<NganWardM>,
+  {"NganWard", 4, kFlagSpecular, &launch_eval_pdf<NganWardM>, &launch_sample<NganWardM>, &launch_reflectance<NganWardM>, &launch_loss<NganWardM>, &launch_check<NganWardM>,
    {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "sssp"},
-  {"NganWardDuer", 4, kFlagSpecular, &launch_eval_pdf<NganWardDuerM>, &launch_sample<NganWardDuerM>, &launch_reflectance<NganWardDuerM>, &launch_loss<NganWardDuerM>,
+  {"NganWardDuer", 4, kFlagSpecular, &launch_eval_pdf<NganWardDuerM>, &launch_sample<NganWardDuerM>, &launch_reflectance<NganWardDuerM>, &launch_loss<NganWardDuerM>, &launch_check<NganWardDuerM>,
    {0.5f, 0.5f, 0.5f, 0.1f}, {0, 0, 0, kEpsF}, {1, 1, 1, 1}, "sssp"},
-  {"Phong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>,
+  {"Phong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>, &launch_check<PhongLobe>,
    {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}, "sssp"},
-  {"NganBlinnPhong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>,   // ngan.h:43-44
+  {"NganBlinnPhong", 4, kFlagSpecular, &launch_eval_pdf<PhongLobe>, &launch_sample<PhongLobe>, &launch_reflectance<PhongLobe>, &launch_loss<PhongLobe>, &launch_check<PhongLobe>,   // ngan.h:43-44
    {0.5f, 0.5f, 0.5f, 32.0f}, {0, 0, 0, 0}, {1, 1, 1, kFMax}, "sssp"},
-  {"Lafortune", 7, kFlagSpecular, &launch_eval_pdf<LafortuneM>, &launch_sample<LafortuneM>, &launch_reflectance<LafortuneM>, &launch_loss<LafortuneM>,
+  {"Lafortune", 7, kFlagSpecular, &launch_eval_pdf<LafortuneM>, &launch_sample<LafortuneM>, &launch_reflectance<LafortuneM>, &launch_loss<LafortuneM>, &launch_check<LafortuneM>,
    {0.5f, 0.5f, 0.5f, -0.57735026919f, -0.57735026919f, 0.57735026919f, 32.0f},
    {0, 0, 0, kFMin, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax, kFMax}, "ssspppp"},
-  {"NganLafortune", 6, kFlagSpecular, &launch_eval_pdf<NganLafortuneM>, &launch_sample<NganLafortuneM>, &launch_reflectance<NganLafortuneM>, &launch_loss<NganLafortuneM>,
+  {"NganLafortune", 6, kFlagSpecular, &launch_eval_pdf<NganLafortuneM>, &launch_sample<NganLafortuneM>, &launch_reflectance<NganLafortuneM>, &launch_loss<NganLafortuneM>, &launch_check<NganLafortuneM>,
    {0.5f, 0.5f, 0.5f, -0.57735026919f, 0.57735026919f, 32.0f}, {0, 0, 0, kFMin, kFMin, 0}, {1, 1, 1, kFMax, kFMax, kFMax}, "sssppp"},
-  {"AshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<ASM>, &launch_sample<ASM>, &launch_reflectance<ASM>, &launch_loss<ASM>,
+  {"AshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<ASM>, &launch_sample<ASM>, &launch_reflectance<ASM>, &launch_loss<ASM>, &launch_check<ASM>,
    {0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, kFMax, kFMax}, "ppppp"},
-  {"AshikhminShirleyFull", 8, kFlagAll, &launch_eval_pdf<ASFullM>, &launch_sample<ASFullM>, &launch_reflectance<ASFullM>, &launch_loss<ASFullM>,
+  {"AshikhminShirleyFull", 8, kFlagAll, &launch_eval_pdf<ASFullM>, &launch_sample<ASFullM>, &launch_reflectance<ASFullM>, &launch_loss<ASFullM>, &launch_check<ASFullM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 0.1f, 0.1f, 32.0f, 32.0f}, {0, 0, 0, 0, 0, 0, 0, 0}, {1, 1, 1, 1, 1, 1, kFMax, kFMax}, "dddppppp"},
-  {"LowAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<LowASM>, &launch_sample<LowASM>, &launch_reflectance<LowASM>, &launch_loss<LowASM>,
+  {"LowAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<LowASM>, &launch_sample<LowASM>, &launch_reflectance<LowASM>, &launch_loss<LowASM>, &launch_check<LowASM>,
    {0.5f, 0.5f, 0.5f, 1.3f, 32.0f}, {0, 0, 0, 1, 0}, {1, 1, 1, 5, kFMax}, "ssspp"},
-  {"NganAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<NganASM>, &launch_sample<NganASM>, &launch_reflectance<NganASM>, &launch_loss<NganASM>,
+  {"NganAshikhminShirley", 5, kFlagSpecular, &launch_eval_pdf<NganASM>, &launch_sample<NganASM>, &launch_reflectance<NganASM>, &launch_loss<NganASM>, &launch_check<NganASM>,
    {0.5f, 0.5f, 0.5f, 0.1f, 32.0f}, {0, 0, 0, 0, 0}, {1, 1, 1, 1, kFMax}, "ssspp"},
-  {"LowSmooth", 6, kFlagSpecular, &launch_eval_pdf<LowSmooth>, &launch_sample<LowSmooth>, &launch_reflectance<LowSmooth>, &launch_loss<LowSmooth>,
+  {"LowSmooth", 6, kFlagSpecular, &launch_eval_pdf<LowSmooth>, &launch_sample<LowSmooth>, &launch_reflectance<LowSmooth>, &launch_loss<LowSmooth>, &launch_check<LowSmooth>,
    {1, 1, 1, 1, 1, 1.3f}, {0, 0, 0, 0, 0, 1}, {kFMax, kFMax, kFMax, kFMax, kFMax, 5}, "pppppp"},
   // bsdfmodel/bagher.h:62-68: albedo, K, Lambda, c, theta0, k (ndf/sgd.h:197-203, Dependent),
   // alpha, p (sgd.h:107-111), eta = (F0, F1) RGB (bagher.h:31, default {1, 0}, lower {0, -1})
-  {"Bagher", 30, kFlagSpecular, &launch_eval_pdf<Bagher>, &launch_sample<Bagher>, &launch_reflectance<Bagher>, &launch_loss<Bagher>,
+  {"Bagher", 30, kFlagSpecular, &launch_eval_pdf<Bagher>, &launch_sample<Bagher>, &launch_reflectance<Bagher>, &launch_loss<Bagher>, &launch_check<Bagher>,
    {0.5f, 0.5f, 0.5f, 7.5f, 7.5f, 7.5f, 1, 1, 1, 1, 1, 1, 1.5707963705062866f, 1.5707963705062866f, 1.5707963705062866f,
     1, 1, 1, 0.1f, 0.1f, 0.1f, 0.64f, 0.64f, 0.64f, 1, 1, 1, 0, 0, 0},
    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, kEpsF, kEpsF, kEpsF, 0, 0, 0, 0, 0, 0, -1, -1, -1},
@@ -143,9 +144,11 @@ struct AggregateSpec
   SampleLauncher sample;
   ReflLauncher reflectance;
   LossLauncher loss;
+  CheckLauncher check;
 };
 #define BBM_HIP_AGG(KEY, CHILD, M) \
-  {KEY, CHILD, kFlagDiffuse | M::kComponent, &launch_eval_pdf<M>, &launch_sample<M>, &launch_reflectance<M>, &launch_loss<M>}
+  {KEY, CHILD, kFlagDiffuse | M::kComponent, &launch_eval_pdf<M>, &launch_sample<M>, &launch_reflectance<M>, &launch_loss<M>, \
+   &launch_check<M>}
 const AggregateSpec kAggregates[] = {
   BBM_HIP_AGG("Aggregate<Lambertian,Bagher>", "Bagher", AggBagherM),                      // fits/bagher_sgd.fit
   BBM_HIP_AGG("Aggregate<Lambertian,CookTorrance>", "CookTorrance", AggCookTorranceM),    // docs/source/fitting.rst:31-33
@@ -185,7 +188,7 @@ struct Registry
       e.name = g.name;
       e.nparams = lam->nparams + c->nparams;
       e.components = g.components;
-      e.eval_pdf = g.eval_pdf; e.sample = g.sample; e.reflectance = g.reflectance; e.loss = g.loss;
+      e.eval_pdf = g.eval_pdf; e.sample = g.sample; e.reflectance = g.reflectance; e.loss = g.loss; e.check = g.check;
       for (int i = 0; i < lam->nparams; ++i)
       {
         e.defaults[i] = lam->defaults[i]; e.lower[i] = lam->lower[i]; e.upper[i] = lam->upper[i];
@@ -236,13 +239,6 @@ int check_dirs(const float* x, const float* y, const float* z, const char* what)
 
 // Counter-based generator: splitmix64 finaliser over (seed, stream, index).  Two 24-bit uniforms
 // per direction.  Pure function of the global index -> shards regenerate identical slices.
-__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z)
-{
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-
 __global__ __launch_bounds__(kBlock) void k_fill_dirs(uint64_t key, uint64_t offset, uint64_t n, int mode,
                                                        float* __restrict__ x, float* __restrict__ y, float* __restrict__ z)
 {
@@ -314,6 +310,76 @@ __global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums,
   }
   if (threadIdx.x == 0) sums[p] = part[0];
 }
+
+// partials [slot][b][kCheckAcc] -> acc[slot][kCheckAcc]: one wave per slot, fixed order
+__global__ __launch_bounds__(64) void k_check_final(const double* partial, int nblocks, double* acc)
+{
+  const int slot = blockIdx.x;
+  double r[kCheckAcc];
+#pragma unroll
+  for (int e = 0; e < kCheckAcc; ++e) r[e] = 0.0;
+  r[kCheckSums] = r[kCheckSums + 2] = -1.0;
+  r[kCheckSums + 1] = r[kCheckSums + 3] = 1.8e19;
+  for (int b = threadIdx.x; b < nblocks; b += 64)
+  {
+    const double* p = partial + (size_t(slot) * nblocks + b) * kCheckAcc;
+#pragma unroll
+    for (int e = 0; e < kCheckSums; ++e) r[e] += p[e];
+    max_pair(r[kCheckSums], r[kCheckSums + 1], p[kCheckSums], p[kCheckSums + 1]);
+    max_pair(r[kCheckSums + 2], r[kCheckSums + 3], p[kCheckSums + 2], p[kCheckSums + 3]);
+  }
+  wave_reduce_check(r);
+  if (threadIdx.x == 0)
+  {
+#pragma unroll
+    for (int e = 0; e < kCheckAcc; ++e) acc[size_t(slot) * kCheckAcc + e] = r[e];
+  }
+}
+
+namespace {
+
+// draw k of a check test: base key of the stream (test, k); the slot is mixed in by check_key
+uint64_t check_base_key(uint64_t seed, int test, int draw)
+{
+  return mix64(seed) ^ (0xd1b54a32d192ed03ull * (uint64_t(0x10000) * uint64_t(test + 1) + uint64_t(draw) + 1));
+}
+
+__global__ __launch_bounds__(kBlock) void k_draws(uint64_t key, uint64_t offset, uint64_t n, float* u0, float* u1)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+    uniform2(key, offset + i, u0[i], u1[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_trials(uint64_t base, int ntrials, int sphere, float* x, float* y, float* z)
+{
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= ntrials) return;
+  float u0, u1;
+  uniform2(check_key(base, t), 0, u0, u1);
+  const v3 d = sphere_dir(u0, u1, sphere == 0);
+  x[t] = d.x; y[t] = d.y; z[t] = d.z;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sphere_dirs(const float* u0, const float* u1, uint64_t n, int hemisphere,
+                                                        float* x, float* y, float* z)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+  {
+    const v3 d = sphere_dir(u0[i], u1[i], hemisphere != 0);
+    x[i] = d.x; y[i] = d.y; z[i] = d.z;
+  }
+}
+
+int launched()
+{
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+  return BBM_HIP_OK;
+}
+
+}  // namespace
 
 }  // namespace bbmhip
 
@@ -545,6 +611,98 @@ int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
   a.block_sums = static_cast<double*>(workspace);
   a.sums = sums;
   return e->loss(a, static_cast<hipStream_t>(stream));
+}
+
+size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* d)
+{
+  if (!d || d->nslots <= 0) return 0;
+  return size_t(d->nslots) * check_blocks(d->n, d->nslots) * kCheckAcc * sizeof(double);
+}
+
+int bbm_hip_check(int model_id, const float* params, int nparams, const bbm_hip_check_desc* d,
+                  double* acc, uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream)
+{
+  const ModelEntry* e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  if (nparams != e->nparams)
+    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
+                                             " parameters, got " + std::to_string(nparams));
+  if (nparams > 0 && !params) return fail(BBM_HIP_ERR_INVALID_ARG, "params is NULL");
+  if (!d) return fail(BBM_HIP_ERR_INVALID_ARG, "check descriptor is NULL");
+  if (d->test < 0 || d->test >= kCheckNumTests) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown check test");
+  if (d->nslots <= 0 || d->nslots > 65535) return fail(BBM_HIP_ERR_INVALID_ARG, "nslots must be in [1, 65535]");
+  const bool chi2 = d->test == kCheckSamplePdf || d->test == kCheckSampleCount;
+  const uint64_t bins = uint64_t(d->theta_bins) * d->phi_bins;
+  if (chi2 && (d->theta_bins == 0 || d->phi_bins == 0 || bins > (1u << 20)))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "theta_bins / phi_bins must be positive (at most 2^20 bins)");
+  if (d->test == kCheckSamplePdf && d->nslots % bins != 0)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "SAMPLE_PDF: nslots must be trials x theta_bins x phi_bins");
+  const bool needs_dirs = d->test == kCheckReflectance || d->test == kCheckPdfInt || chi2;
+  if (needs_dirs && (!d->slot_x || !d->slot_y || !d->slot_z))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "this test needs slot directions");
+  if (d->test == kCheckSampleCount ? !counts : !acc) return fail(BBM_HIP_ERR_INVALID_ARG, "acc / counts pointer is NULL");
+  if (d->test != kCheckSampleCount && (!workspace || workspace_bytes < bbm_hip_check_workspace_size(d)))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "workspace too small (bbm_hip_check_workspace_size)");
+  CheckArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int k = 0; k < 3; ++k) a.key[k] = check_base_key(d->seed, d->test, k);
+  a.begin = d->begin; a.n = d->n; a.nslots = d->nslots;
+  a.sx = d->slot_x; a.sy = d->slot_y; a.sz = d->slot_z;
+  a.sphere = d->sphere; a.importance = d->importance; a.include_zero = d->include_zero_pdf;
+  a.nth = d->theta_bins; a.nph = d->phi_bins;
+  a.partial = static_cast<double*>(workspace);
+  a.counts = reinterpret_cast<unsigned long long*>(counts);
+  for (int i = 0; i < nparams; ++i) a.p.v[i] = params[i];
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (d->test == kCheckSampleCount)
+  {
+    const hipError_t me = hipMemsetAsync(counts, 0, size_t(d->nslots) * bins * sizeof(uint64_t), s);
+    if (me != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(me));
+  }
+  if (d->n == 0 && d->test != kCheckSampleCount)
+  {
+    const hipError_t me = hipMemsetAsync(acc, 0, size_t(d->nslots) * kCheckAcc * sizeof(double), s);
+    return me == hipSuccess ? BBM_HIP_OK : fail(BBM_HIP_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(me));
+  }
+  if (d->n == 0) return BBM_HIP_OK;
+  return e->check(d->test, a, acc, s);
+}
+
+int bbm_hip_check_draws(int test, uint64_t seed, int slot, int draw, uint64_t offset, size_t n,
+                        float* xi0, float* xi1, void* stream)
+{
+  if (n == 0) return BBM_HIP_OK;
+  if (!xi0 || !xi1) return fail(BBM_HIP_ERR_INVALID_ARG, "xi pointer is NULL");
+  if (test < 0 || test >= kCheckNumTests || draw < 0 || draw > 2 || slot < 0)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "test / draw / slot out of range");
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipLaunchKernelGGL(k_draws, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     check_key(check_base_key(seed, test, draw), slot), offset, uint64_t(n), xi0, xi1);
+  return launched();
+}
+
+int bbm_hip_check_trials(int test, uint64_t seed, int ntrials, int sphere, float* x, float* y, float* z, void* stream)
+{
+  if (ntrials <= 0) return ntrials == 0 ? BBM_HIP_OK : fail(BBM_HIP_ERR_INVALID_ARG, "ntrials < 0");
+  if (!x || !y || !z) return fail(BBM_HIP_ERR_INVALID_ARG, "direction pointer is NULL");
+  if (test < 0 || test >= kCheckNumTests) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown check test");
+  // the trial direction is its own stream (draw index 3), sample 0
+  hipLaunchKernelGGL(k_trials, dim3(unsigned((ntrials + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), check_base_key(seed, test, 3), ntrials, sphere, x, y, z);
+  return launched();
+}
+
+int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisphere, float* x, float* y, float* z,
+                        void* stream)
+{
+  if (n == 0) return BBM_HIP_OK;
+  if (!xi0 || !xi1 || !x || !y || !z) return fail(BBM_HIP_ERR_INVALID_ARG, "pointer is NULL");
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipLaunchKernelGGL(k_sphere_dirs, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), xi0, xi1,
+                     uint64_t(n), hemisphere, x, y, z);
+  return launched();
 }
 
 int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,

@@ -558,7 +558,14 @@ int launch_loss(const LossArgs& a0, hipStream_t s)
   return BBM_HIP_OK;
 }
 
+}  // namespace bbmhip
+
+#include "check.hpp"
+
+namespace bbmhip {
+
 using LossLauncher = int (*)(const LossArgs&, hipStream_t);
+using CheckLauncher = int (*)(int, const CheckArgs&, double*, hipStream_t);
 using EvalLauncher = int (*)(const EvalArgs&, int, hipStream_t);
 using SampleLauncher = int (*)(const SampleArgs&, hipStream_t);
 using ReflLauncher = int (*)(const ReflArgs&, hipStream_t);

@@ -31,6 +31,15 @@ constexpr float kPi8F = float(8.0f * kPiD);          // Constants::Pi(8)
 constexpr float kInvPiHalfF = float(0.5f * kInvPiD); // Constants::InvPi(0.5)
 constexpr float kEpsF = 1.1920928955078125e-07f;   // numeric_limits<float>::epsilon()
 
+// splitmix64 finaliser: the counter-based generators (synthetic directions, checkBsdf draws) hash
+// (key + golden-ratio * index), so element i of a stream is a pure function of its global index.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
 struct v3 { float x, y, z; };
 struct v2 { float x, y; };
 

@@ -68,9 +68,11 @@ using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
   template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);           \
   template int launch_sample<M>(const SampleArgs&, hipStream_t);                \
   template int launch_reflectance<M>(const ReflArgs&, hipStream_t);            \
-  template int launch_loss<M>(const LossArgs&, hipStream_t);
+  template int launch_loss<M>(const LossArgs&, hipStream_t);                  \
+  template int launch_check<M>(int, const CheckArgs&, double*, hipStream_t);
 #define BBM_HIP_EXTERN(M)                                                        \
   extern template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);    \
   extern template int launch_sample<M>(const SampleArgs&, hipStream_t);         \
   extern template int launch_reflectance<M>(const ReflArgs&, hipStream_t);     \
-  extern template int launch_loss<M>(const LossArgs&, hipStream_t);
+  extern template int launch_loss<M>(const LossArgs&, hipStream_t);           \
+  extern template int launch_check<M>(int, const CheckArgs&, double*, hipStream_t);

@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--model", default="CookTorrance")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit"],
+                    help="evalpdf: the BASELINE metric (config 2, default); models: every model's eval over shared "
+                         "pairs (config 3); sample: importance-sample -> eval -> pdf MC loop (config 4); fit: "
+                         "multi-probe fitting loss of a compass step over the MERL grid (config 5)")
     return ap.parse_args()
 
 
@@ -104,6 +108,12 @@ def main():
         torch.cuda.set_device(0)
 
     import bbm_amd
+    if args.workload != "evalpdf":
+        from tools import bench_configs
+        bench_configs.run(args, dist, rank, world)
+        if dist:
+            dist.destroy_process_group()
+        return
     model = bbm_amd.BsdfModel(args.model)
     n = args.pairs
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 2
+#define BBM_HIP_ABI_VERSION 3
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -179,6 +179,70 @@ int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
  * stream_id selects an independent stream of the generator (e.g. 0 = in, 1 = out). */
 int bbm_hip_fill_directions(uint64_t seed, uint32_t stream_id, uint64_t offset, size_t n, int mode,
                             float* x, float* y, float* z, void* stream);
+
+/* ---------------------------------------------------------------- checkBsdf statistics */
+
+/* bin/checkBsdf.cpp's tests (:51-418) as batched reductions over n random samples per slot.
+ * Random numbers: counter-based (bbm_hip_check_draws), one stream per (test, slot, draw), so a
+ * shard [begin, begin + n) of the samples draws exactly what one GPU would have drawn for them.
+ * Accumulators are double; acc (device) receives nslots x BBM_CHECK_ACC doubles, laid out per test:
+ *   REFLECTANCE (:51-97)   slot = theta_out (slot direction = out): [0..2] sum eval(dir, out) z(dir) / pdf,
+ *                          [3] accepted samples (pdf > eps); importance != 0 samples the BSDF, else sampleSphere
+ *   RECIPROCITY (:102-140) [0..2] sum |f(in,out) - f(out,in)| Radiance, [3..5] Importance,
+ *                          [8] max hsum (Radiance) at sample [9], [10] max hsum (Importance) at sample [11]
+ *   ADJOINT (:145-185)     [0..2] sum |f_Radiance(in,out) - f_Importance(out,in)|, [8] max hsum at sample [9]
+ *   PDF (:190-245)         [0]/[1] negative pdf (Radiance/Importance), [2]/[3] sampled below the horizon,
+ *                          [4]/[5] sum |sample.pdf - pdf(sample.direction, out)|; out on the hemisphere
+ *                          (sphere != 0: sphere)
+ *   PDFINT (:250-290)      slot = trial (slot direction = trial direction): [0]/[1] sum pdf(dir, t) / (1 / 4 pi)
+ *   SAMPLE_PDF (:330-357)  slot = trial * bins + bin (slot directions = trial directions, one per trial):
+ *                          [0] sum pdf(dir, t) * solid angle weight over the bin's n pdf samples
+ *   SAMPLE_COUNT (:360-380) slot = trial: counts[slot][bin] = samples landing in the (theta, phi) bin
+ *                          (pdf > eps unless include_zero_pdf); acc unused, counts zeroed by the call.
+ * The caller divides by the sample counts (after summing shards across GPUs). */
+#define BBM_CHECK_REFLECTANCE 0
+#define BBM_CHECK_RECIPROCITY 1
+#define BBM_CHECK_ADJOINT 2
+#define BBM_CHECK_PDF 3
+#define BBM_CHECK_PDFINT 4
+#define BBM_CHECK_SAMPLE_PDF 5
+#define BBM_CHECK_SAMPLE_COUNT 6
+#define BBM_CHECK_ACC 12
+
+typedef struct bbm_hip_check_desc
+{
+  int32_t test;
+  int32_t nslots;
+  uint64_t seed;
+  uint64_t begin, n;                 /* samples [begin, begin + n) of every slot */
+  const float* slot_x;               /* device, per-slot direction (see above); NULL where unused */
+  const float* slot_y;
+  const float* slot_z;
+  int32_t sphere;                    /* PDF: out uniform on the sphere instead of the hemisphere */
+  int32_t importance;                /* REFLECTANCE: importance sampling */
+  int32_t include_zero_pdf;          /* SAMPLE_COUNT: includeZeroPdfSamples */
+  uint32_t theta_bins, phi_bins;     /* SAMPLE_PDF / SAMPLE_COUNT */
+} bbm_hip_check_desc;
+
+/* Workspace (bytes, device memory) bbm_hip_check needs for this descriptor. */
+size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* desc);
+
+/* Run one checkBsdf statistic of model_id (params uniform) -> acc / counts (device). */
+int bbm_hip_check(int model_id, const float* params, int nparams, const bbm_hip_check_desc* desc,
+                  double* acc, uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+
+/* The uniforms draw `draw` (0..2) of slot `slot` of `test` uses for samples offset .. offset + n - 1
+ * (rndVec2d(), checkBsdf.cpp:21-26): xi0[i], xi1[i] in [0, 1), 24-bit. */
+int bbm_hip_check_draws(int test, uint64_t seed, int slot, int draw, uint64_t offset, size_t n,
+                        float* xi0, float* xi1, void* stream);
+
+/* Trial directions of PDFINT / SAMPLE_PDF / SAMPLE_COUNT: trial t = sampleHemisphere (sphere = 0) or
+ * sampleSphere (sphere != 0) of its own draw (checkBsdf.cpp:270, :322). */
+int bbm_hip_check_trials(int test, uint64_t seed, int ntrials, int sphere, float* x, float* y, float* z, void* stream);
+
+/* sampleSphere / sampleHemisphere (checkBsdf.cpp:28-45) of n uniform pairs (device). */
+int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisphere, float* x, float* y, float* z,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -3,3 +3,4 @@
  * so the shim's parts must share one translation unit. */
 #include "ref_harness.cpp"
 #include "ref_fit.cpp"
+#include "ref_check.cpp"

@@ -1,0 +1,160 @@
+"""bench.py --workload models|sample|fit: BASELINE.json configs 3-5 (one JSON line each).
+
+  models  (config 3) every single bsdfmodel's eval over 10M shared pairs per GPU, one launch per model
+          (bbm_hip_eval).  Algorithmic bytes: 24 B in + 12 B RGB out = 36 B/pair (models that read only
+          z: 8 + 12 = 20 B).  Per-model pairs/s and fraction of the 8 TB/s HBM roofline.
+  sample  (config 4) importance-sample -> eval -> pdf Monte-Carlo loop (checkBsdf's reflectance test,
+          bbm_hip_check REFLECTANCE with importance sampling) for the microfacet models CookTorrance and
+          GGX: 125M samples per GPU (1B over 8 GPUs), 8 theta_out slots, reduced in-kernel to per-slot
+          sums -- no HBM traffic per sample, so the kernel is VALU-bound: reported as samples/s.
+  fit     (config 5) the fitting loss of one compass step: Aggregate(Lambertian, Bagher) against a
+          reference table on the MERL grid (90 x 90 x 180 = 1.458M pairs, sharded over the GPUs),
+          2P = 36 probes in one bbm_hip_loss launch, plus the RCCL all-reduce of the 36 partial sums
+          when N > 1 (strong scaling: the grid is fixed).  Reported as probe-pair evaluations/s.
+Timing follows bench.py: warmup, barrier + synchronize around K timed steps, max over ranks.
+"""
+import ctypes
+import json
+import time
+
+import numpy as np
+import torch
+
+import bbm_amd
+from bbm_amd import _lib, check, fit
+from bbm_amd.backbone import _stream_ptr
+
+SEED = 0xBB5EED
+HBM_PEAK_GBS = 8000.0
+Z_ONLY = {"Lambertian"}
+
+
+def _timed(step, args, dist, stream):
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < args.settle_s:
+        step()
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def _line(args, world, metric, value, unit, elapsed, config, extra):
+    d = {"metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
+         "data": "synthetic", "config": config}
+    d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def bench_models(args, dist, rank, world):
+    n = 10_000_000
+    din = bbm_amd.fill_directions(SEED, 0, rank * n, n, mode=0)
+    dout = bbm_amd.fill_directions(SEED, 1, rank * n, n, mode=0)
+    rgb = torch.empty((3, n), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    per = {}
+    total_t = 0.0
+    names = [m for m in bbm_amd.model_names() if not m.startswith("Aggregate")]
+    for name in names:
+        m = bbm_amd.BsdfModel(name)
+        elapsed, kern_ms = _timed(lambda: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=stream), args, dist, stream)
+        bpp = 20 if name in Z_ONLY else 36
+        gbs = bpp * n / (kern_ms * 1e-3) / 1e9
+        per[name] = {"pairs_per_s": n * world * args.steps / elapsed, "kernel_ms": kern_ms, "GB_s": gbs,
+                     "roofline_frac": gbs / HBM_PEAK_GBS, "bytes_per_pair": bpp}
+        total_t += elapsed
+    if rank == 0:
+        _line(args, world, "BSDF evals/s (eval), all single bsdfmodels, 10M shared pairs per GPU (config 3)",
+              len(names) * n * world * args.steps / total_t, "pairs/s", total_t / len(names),
+              {"workload": f"{len(names)} models x eval over {n} shared pairs per GPU, one kernel per model",
+               "pairs_per_gpu": n, "parallelism": f"dp{world} (independent shards)"},
+              {"scaling": "weak", "per_model": per})
+
+
+def bench_sample(args, dist, rank, world):
+    per_gpu = 125_000_000
+    slots = 8
+    lib = _lib.load()
+    outs = torch.from_numpy(check.reflectance_outs(slots)).cuda()
+    stream = torch.cuda.current_stream()
+    res = {}
+    total_t = 0.0
+    for name in ("CookTorrance", "GGX"):
+        m = bbm_amd.BsdfModel(name)
+        d = check.CheckDesc()
+        d.test, d.nslots, d.seed, d.begin, d.n = check.REFLECTANCE, slots, SEED, rank * (per_gpu // slots), per_gpu // slots
+        d.slot_x, d.slot_y, d.slot_z = outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr()
+        d.importance = 1
+        acc = torch.empty((slots, check.ACC), dtype=torch.float64, device="cuda")
+        wsb = int(lib.bbm_hip_check_workspace_size(ctypes.byref(d)))
+        ws = torch.empty(max(wsb // 8, 1), dtype=torch.float64, device="cuda")
+
+        def step():
+            _lib.check(lib.bbm_hip_check(m.model_id, m._pptr(), m._params.size, ctypes.byref(d), acc.data_ptr(), None,
+                                         ws.data_ptr(), wsb, _stream_ptr(stream)))
+
+        elapsed, kern_ms = _timed(step, args, dist, stream)
+        a = check._gather_acc(acc.cpu().numpy(), dist)
+        total = (per_gpu // slots) * slots * world
+        est = a[:, :3] / float(total // slots)
+        refl = m.reflectance(outs).cpu().numpy().T
+        res[name] = {"samples_per_s": total * args.steps / elapsed, "kernel_ms": kern_ms,
+                     "estimate_vs_reflectance": [[float(x) for x in est[k]] + [float(y) for y in refl[k]] for k in (0, slots - 1)]}
+        total_t += elapsed
+    if rank == 0:
+        tot = 2 * (per_gpu // slots) * slots * world * args.steps
+        _line(args, world, "importance-sample->eval->pdf samples/s, microfacet (CookTorrance, GGX), 125M samples per GPU "
+              "(config 4)", tot / total_t, "samples/s", total_t / 2,
+              {"workload": f"checkBsdf reflectance test, importance sampling, {slots} theta_out x "
+                           f"{per_gpu // slots} samples per GPU, in-kernel reduction",
+               "samples_per_gpu": per_gpu, "parallelism": f"dp{world} (sample shards, one gather at the end)"},
+              {"scaling": "weak", "per_model": res, "roofline": {"bound": "valu", "note": "no per-sample HBM traffic"}})
+
+
+def bench_fit(args, dist, rank, world):
+    name = "Aggregate<Lambertian,Bagher>"
+    fitted = bbm_amd.BsdfModel(name)
+    reference = bbm_amd.BsdfModel(name)
+    p = reference.parameter_values()
+    reference.set_parameter_values((p * np.float32(1.1)).astype(np.float32))
+    lin = fit.merl_linearizer()
+    loss = fit.SampledLoss(fitted, reference, "standardLog", lin, dist=dist)
+    idx = fitted.parameter_indices(fit.ALL)
+    probes = np.repeat(fitted.parameter_values()[None], 2 * len(idx), axis=0)
+    for k, j in enumerate(idx):
+        probes[2 * k, j] *= np.float32(1.01)
+        probes[2 * k + 1, j] *= np.float32(0.99)
+    stream = torch.cuda.current_stream()
+    elapsed, kern_ms = _timed(lambda: loss.probe_sums(probes), args, dist, stream)
+    if rank == 0:
+        pairs = lin.size()
+        _line(args, world, "fitting-loss probe-pair evals/s, Aggregate(Lambertian, Bagher), MERL grid, 2P probes per "
+              "compass step (config 5)", len(probes) * pairs * args.steps / elapsed, "probe-pairs/s", elapsed,
+              {"workload": f"{len(probes)} probes x {pairs} MERL pairs per compass step (standardLog), sharded grid",
+               "probes": len(probes), "pairs": pairs, "parallelism": f"dp{world} (grid shards, all-reduce of "
+                                                                      f"{len(probes)} doubles per step)"},
+              {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms})
+
+
+def run(args, dist, rank, world):
+    {"models": bench_models, "sample": bench_sample, "fit": bench_fit}[args.workload](args, dist, rank, world)
