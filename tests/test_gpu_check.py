@@ -93,12 +93,15 @@ def test_reciprocity_and_adjoint_match_reference(chk, name, test):
     # scale: the magnitude of the evaluated values (differences of a reciprocal model are round-off)
     din, _ = co.sphere_dirs(co.draws(test, SEED, 0, 0, 0, n))
     dout, _ = co.sphere_dirs(co.draws(test, SEED, 0, 1, 0, n))
-    scale = np.abs(ou.ref_eval_pdf(name, m.parameter_values(), din, dout, nthreads=8)[:3]).sum(dtype=np.float64)
+    f = np.abs(ou.ref_eval_pdf(name, m.parameter_values(), din, dout, nthreads=8)[:3]).astype(np.float64)
+    scale = f.sum()
     for c in range(3):
         _close(acc[c], sums[c], scale, 1e-5, f"{name} sum {c}")
         if test == 1:
             assert acc[3 + c] == acc[c]
-    assert abs(max(acc[8], 0.0) - hmax) <= 1e-5 * scale / n * 100 + 1e-6 * hmax
+    # the largest difference: each value is within 1e-5 of the reference's, so the maximum is within
+    # 1e-5 of the largest value's magnitude (a non-reciprocal model's maximum need not be unique)
+    assert abs(max(acc[8], 0.0) - hmax) <= 2e-5 * f.sum(axis=0).max() + 1e-6 * hmax, (acc[8], hmax)
 
 
 @pytest.mark.parametrize("name", MODELS)
