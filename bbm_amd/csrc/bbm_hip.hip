@@ -581,6 +581,33 @@ size_t bbm_hip_loss_workspace_size(int nprobes)
   return nprobes > 0 ? size_t(kLossMaxBlocks) * size_t(nprobes) * sizeof(double) : 0;
 }
 
+namespace {
+int loss_common(int model_id, const float* probes, int nparams, int nprobes, const float* ref_r, const float* ref_g,
+                const float* ref_b, size_t n, int loss_kind, uint32_t component, double* sums, void* workspace,
+                size_t workspace_bytes, LossArgs& a, const ModelEntry*& e)
+{
+  e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  if (nparams != e->nparams)
+    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
+                                             " parameters, got " + std::to_string(nparams));
+  if (nprobes <= 0) return fail(BBM_HIP_ERR_INVALID_ARG, "nprobes must be positive");
+  if (loss_kind < BBM_LOSS_NGAN_L2 || loss_kind > BBM_LOSS_BIERON_LOG) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown loss kind");
+  if (!probes || !sums) return fail(BBM_HIP_ERR_INVALID_ARG, "probes / sums pointer is NULL");
+  if (n > 0 && (!ref_r || !ref_g || !ref_b)) return fail(BBM_HIP_ERR_INVALID_ARG, "reference pointer is NULL");
+  if (!workspace || workspace_bytes < bbm_hip_loss_workspace_size(nprobes))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "workspace too small (bbm_hip_loss_workspace_size)");
+  std::memset(&a, 0, sizeof(a));
+  a.n = n;
+  a.ref_r = ref_r; a.ref_g = ref_g; a.ref_b = ref_b;
+  a.probes = probes; a.nprobes = nprobes; a.stride = nparams; a.loss_kind = loss_kind;
+  a.component = component & kFlagAll;
+  a.block_sums = static_cast<double*>(workspace);
+  a.sums = sums;
+  return BBM_HIP_OK;
+}
+}  // namespace
+
 int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
                  const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
                  const float* ref_r, const float* ref_g, const float* ref_b,
@@ -588,28 +615,38 @@ int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
                  double* sums, void* workspace, size_t workspace_bytes, void* stream)
 {
   (void)unit;
-  const ModelEntry* e = entry(model_id);
-  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
-  if (nparams != e->nparams)
-    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
-                                             " parameters, got " + std::to_string(nparams));
-  if (nprobes <= 0) return fail(BBM_HIP_ERR_INVALID_ARG, "nprobes must be positive");
-  if (loss_kind < BBM_LOSS_NGAN_L2 || loss_kind > BBM_LOSS_BIERON_LOG) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown loss kind");
-  LossArgs a;
-  std::memset(&a, 0, sizeof(a));
-  int rc = to_desc(lin, a.lin);
+  LinDesc d;
+  int rc = to_desc(lin, d);
   if (rc) return rc;
-  if (begin + n > lin_size(a.lin)) return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer range out of bounds");
-  if (!probes || !sums) return fail(BBM_HIP_ERR_INVALID_ARG, "probes / sums pointer is NULL");
-  if (n > 0 && (!ref_r || !ref_g || !ref_b)) return fail(BBM_HIP_ERR_INVALID_ARG, "reference pointer is NULL");
-  if (!workspace || workspace_bytes < bbm_hip_loss_workspace_size(nprobes))
-    return fail(BBM_HIP_ERR_INVALID_ARG, "workspace too small (bbm_hip_loss_workspace_size)");
-  a.begin = begin; a.n = n;
-  a.ref_r = ref_r; a.ref_g = ref_g; a.ref_b = ref_b;
-  a.probes = probes; a.nprobes = nprobes; a.stride = nparams; a.loss_kind = loss_kind;
-  a.component = component & kFlagAll;
-  a.block_sums = static_cast<double*>(workspace);
-  a.sums = sums;
+  if (begin + n > lin_size(d)) return fail(BBM_HIP_ERR_INVALID_ARG, "linearizer range out of bounds");
+  LossArgs a;
+  const ModelEntry* e = nullptr;
+  rc = loss_common(model_id, probes, nparams, nprobes, ref_r, ref_g, ref_b, n, loss_kind, component, sums, workspace,
+                   workspace_bytes, a, e);
+  if (rc) return rc;
+  a.lin = d;
+  a.begin = begin;
+  return e->loss(a, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprobes, size_t n,
+                       const float* in_x, const float* in_y, const float* in_z,
+                       const float* out_x, const float* out_y, const float* out_z,
+                       const float* ref_r, const float* ref_g, const float* ref_b,
+                       int loss_kind, uint32_t component, uint32_t unit,
+                       double* sums, void* workspace, size_t workspace_bytes, void* stream)
+{
+  (void)unit;
+  LossArgs a;
+  const ModelEntry* e = nullptr;
+  int rc = loss_common(model_id, probes, nparams, nprobes, ref_r, ref_g, ref_b, n, loss_kind, component, sums, workspace,
+                       workspace_bytes, a, e);
+  if (rc) return rc;
+  if (n > 0 && (!in_x || !in_y || !in_z || !out_x || !out_y || !out_z))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "direction pointer is NULL");
+  a.lin.kind = kLinSpherical;    // unused: the pairs are given
+  a.pairs[0] = in_x; a.pairs[1] = in_y; a.pairs[2] = in_z;
+  a.pairs[3] = out_x; a.pairs[4] = out_y; a.pairs[5] = out_z;
   return e->loss(a, static_cast<hipStream_t>(stream));
 }
 

@@ -158,7 +158,7 @@ __device__ __forceinline__ LossSample loss_prepare(int kind, v3 in, v3 out, cons
   for (int k = 0; k < 3; ++k)
   {
     s.r[k] = ref[k];
-    s.lr[k] = (kind >= kLossStandardLog) ? logf_cr(1 + ref[k] * s.c) : 0.0f;
+    s.lr[k] = (kind >= kLossStandardLog) ? logf(1 + ref[k] * s.c) : 0.0f;   // same log as the fitted side
   }
   return s;
 }
@@ -183,7 +183,9 @@ __device__ __forceinline__ float sample_loss(int kind, const LossSample& s, cons
 #pragma unroll
     for (int k = 0; k < 3; ++k)
     {
-      const double e = double(logf_cr(1 + v[k] * s.c) - s.lr[k]);
+      // std::log(float): the device logf (v_log_f32 + extended-precision ln 2 scaling, ~1 ulp, 14 VALU,
+      // vs ~100 for a log rounded from f64) on both sides, so fitted == reference gives exactly 0
+      const double e = double(logf(1 + v[k] * s.c) - s.lr[k]);
       h = h + e * e;
     }
   }

@@ -473,13 +473,14 @@ int launch_reflectance(const ReflArgs& a, hipStream_t s)
 
 // ------------------------------------------------------------------------- fitting loss
 
-constexpr int kProbeBatch = 8;          // probes evaluated per pass over the samples (f64 accumulators)
+constexpr int kProbeBatch = 12;         // probes evaluated per pass over the samples (f64 accumulators)
 constexpr int kLossMaxBlocks = 2048;    // workspace = kLossMaxBlocks x nprobes doubles
 
 struct LossArgs
 {
   LinDesc lin;
   uint64_t begin, n;                    // samples [begin, begin + n) of the linearizer
+  const float* pairs[6];                // or: the pairs themselves (in xyz, out xyz; pairs[0] == NULL: use lin)
   const float* ref_r; const float* ref_g; const float* ref_b;   // reference value of sample begin + i
   const float* probes;                  // nprobes x stride parameter vectors (device)
   int nprobes, stride, loss_kind;
@@ -509,7 +510,12 @@ __global__ __launch_bounds__(kBlock) void k_loss(LossArgs a)
     for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
     {
       v3 in, out;
-      lin_pair(a.lin, a.begin + i, in, out);
+      if (a.pairs[0] != nullptr)
+      {
+        in = mk3(a.pairs[0][i], a.pairs[1][i], a.pairs[2][i]);
+        out = mk3(a.pairs[3][i], a.pairs[4][i], a.pairs[5][i]);
+      }
+      else lin_pair(a.lin, a.begin + i, in, out);
       const float ref[3] = {a.ref_r[i], a.ref_g[i], a.ref_b[i]};
       const LossSample s = loss_prepare(a.loss_kind, in, out, ref);
 #pragma unroll

@@ -487,7 +487,7 @@ struct LowSmooth
     {
       const float dp2 = sqnorm2(in.x + out.x, in.y + out.y);
       const float cosD = float(safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y)));
-      const float S = float(pow(1.0 + B * dp2, double(-C)));
+      const float S = powf_pos(float(1.0 + B * dp2), -C);     // double pow in the reference; see LowNdf::eval
       const float Q = fres.eval(cosD);
 #pragma unroll
       for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0f;

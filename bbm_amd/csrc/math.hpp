@@ -194,6 +194,11 @@ __device__ __forceinline__ float pow2f(float x) { return x * x; }
 // 1-ulp expf difference is not amplified; the eval kernels keep the full-rate f32 expf.
 __device__ __forceinline__ float expf_cr(float x) { return float(exp(double(x))); }
 __device__ __forceinline__ float logf_cr(float x) { return float(log(double(x))); }
+// x^y for x > 0 on the transcendental unit: exp2(y log2 x), v_log_f32 + v_exp_f32 (each ~1 ulp).
+// Relative error ~ (1 + |y log2 x|) * 2^-23: below 3e-6 wherever the result is a normal float that
+// matters (|y log2 x| < 25), vs ~100 VALU instructions for the library powf.  x <= 0 gives NaN / 0 / inf
+// like exp2(y * log2(x)); callers select those lanes away.
+__device__ __forceinline__ float powf_pos(float x, float y) { return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x)); }
 // glibc powf (what std::pow(float, float) calls) is computed in double and rounded once; so is this
 __device__ __forceinline__ float powf_cr(float x, float y) { return float(pow(double(x), double(y))); }
 

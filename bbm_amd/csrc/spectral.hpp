@@ -17,8 +17,10 @@
 
 namespace bbmhip {
 
-// spherical::theta(v) for z(v) >= 0 (include/core/spherical.h:26-32):
-// 2.0 * asin(0.5 * |v - (0,0,sign(z))|) in double, returned as float; for z < 0, Pi - that.
+// spherical::theta(v) (include/core/spherical.h:26-32): 2.0 * asin(0.5 * |v - (0,0,sign(z))|), evaluated
+// by the reference in double and returned as float; for z < 0, Pi - that.  theta_of keeps that (the
+// linearizers, checkBsdf binning and the Bagher shadowing term use it -- the latter is so ill-conditioned
+// for published fits that a 1-ulp different theta moves G by 1e-2, so theta is rounded from f64 as there).
 __device__ __forceinline__ float theta_of(v3 v)
 {
   const float sz = (v.z < 0.0f) ? -1.0f : 1.0f;          // bbm::sign = copysign(1, z)
@@ -50,6 +52,8 @@ struct Bagher
   // ndf::sgd::G1 per channel (ndf/sgd.h:157-193), for a direction with theta(v) = th
   __device__ __forceinline__ float G1(int j, float th) const
   {
+    // 1 + Lambda (1 - exp(c pow(...))) cancels catastrophically for published fits (fits/bagher_sgd.fit:
+    // k ~ 48, c ~ 1e-7 -> g ~ 5e-4 at grazing angles): pow and theta must round like the reference's
     const float g = 1.0f + Lambda[j] * (1.0f - expf(c[j] * powf(th - theta0[j], k[j])));
     return (th > theta0[j]) ? g : 1.0f;
   }
@@ -77,7 +81,9 @@ struct Bagher
       {
         // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
         const float t = alpha[j] + div_nr(tan2, alpha[j]);
-        const float den = powf(t, p[j]);
+        // exp(-t) / t^p is well conditioned: exp2(p log2 t) on the transcendental unit (relative error
+        // ~(1 + |p log2 t|) 2^-23) instead of the 173-instruction library powf
+        const float den = powf_pos(t, p[j]);
         const float P22 = (den > kEpsF) ? div_nr(expf(-t), den) : 0.0f;
         const float Dj = ((h.z > 0) ? f_div_d(double(P22), dnorm) : 0.0f) * K[j];
         const float Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0f;

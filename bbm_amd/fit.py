@@ -108,7 +108,7 @@ class SampledLoss:
     once into a table on this rank's shard) or a (3, n_shard) CUDA tensor of reference values.
     dist: torch.distributed module (or None); the shard is this rank's part of the grid."""
 
-    def __init__(self, fitted, reference, loss, lin, component=3, unit=0, dist=None, stream=None):
+    def __init__(self, fitted, reference, loss, lin, component=3, unit=0, dist=None, stream=None, materialize=True):
         torch = _torch()
         self.fitted = fitted
         self.loss_kind = LOSS_NAMES[loss] if isinstance(loss, str) else int(loss)
@@ -120,8 +120,14 @@ class SampledLoss:
         rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
         self.begin, end = shard_range(self.total, rank, world)
         self.n = end - self.begin
+        # materialize: the shard's direction pairs are computed once (bbm_hip_linearize, 24 B/sample resident)
+        # and every compass step streams them (bbm_hip_loss_pairs) instead of recomputing the linearizer
+        self.pairs = lin.directions(self.begin, self.n, stream) if materialize else None
         if hasattr(reference, "eval"):
-            self.ref = reference_table(reference, lin, self.begin, self.n, stream)
+            if self.pairs is not None:
+                self.ref = reference.eval(self.pairs[0], self.pairs[1], stream=stream)
+            else:
+                self.ref = reference_table(reference, lin, self.begin, self.n, stream)
         else:
             self.ref = reference
         if self.ref.shape != (3, self.n):
@@ -158,10 +164,20 @@ class SampledLoss:
         dp = torch.from_numpy(p).to(self.dev, non_blocking=False)
         sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
         ws = self._workspace(nprobes)
-        _lib.check(_lib.load().bbm_hip_loss(self.fitted.model_id, dp.data_ptr(), npar, nprobes, ctypes.byref(self.lin),
-                                            self.begin, self.n, self.ref[0].data_ptr(), self.ref[1].data_ptr(),
-                                            self.ref[2].data_ptr(), self.loss_kind, self.component, self.unit,
-                                            sums.data_ptr(), ws.data_ptr(), ws.numel() * 8, _stream_ptr(self.stream)))
+        lib = _lib.load()
+        if self.pairs is not None:
+            din, dout = self.pairs
+            _lib.check(lib.bbm_hip_loss_pairs(self.fitted.model_id, dp.data_ptr(), npar, nprobes, self.n,
+                                              din[0].data_ptr(), din[1].data_ptr(), din[2].data_ptr(),
+                                              dout[0].data_ptr(), dout[1].data_ptr(), dout[2].data_ptr(),
+                                              self.ref[0].data_ptr(), self.ref[1].data_ptr(), self.ref[2].data_ptr(),
+                                              self.loss_kind, self.component, self.unit, sums.data_ptr(), ws.data_ptr(),
+                                              ws.numel() * 8, _stream_ptr(self.stream)))
+        else:
+            _lib.check(lib.bbm_hip_loss(self.fitted.model_id, dp.data_ptr(), npar, nprobes, ctypes.byref(self.lin),
+                                        self.begin, self.n, self.ref[0].data_ptr(), self.ref[1].data_ptr(),
+                                        self.ref[2].data_ptr(), self.loss_kind, self.component, self.unit,
+                                        sums.data_ptr(), ws.data_ptr(), ws.numel() * 8, _stream_ptr(self.stream)))
         self.launches += 1
         return sums
 

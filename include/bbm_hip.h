@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 3
+#define BBM_HIP_ABI_VERSION 4
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -169,6 +169,17 @@ int bbm_hip_loss(int model_id, const float* probes, int nparams, int nprobes,
                  const float* ref_r, const float* ref_g, const float* ref_b,
                  int loss_kind, uint32_t component, uint32_t unit,
                  double* sums, void* workspace, size_t workspace_bytes, void* stream);
+
+/* bbm_hip_loss over n caller-provided direction pairs (a linearizer materialised once, e.g. with
+ * bbm_hip_linearize, or any table of measured directions): the pair of sample i is (in[i], out[i]) and its
+ * reference value ref[i].  Same probes / sums / workspace conventions as bbm_hip_loss; the fitting loop
+ * reads 36 B per sample per pass instead of recomputing the linearizer's trigonometry. */
+int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprobes, size_t n,
+                       const float* in_x, const float* in_y, const float* in_z,
+                       const float* out_x, const float* out_y, const float* out_z,
+                       const float* ref_r, const float* ref_g, const float* ref_b,
+                       int loss_kind, uint32_t component, uint32_t unit,
+                       double* sums, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- synthetic directions */
 

@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 3
+    assert lib.bbm_hip_abi_version() == 4
 
 
 def test_registry_matches_reference(lib):

@@ -170,6 +170,7 @@ def test_shard_sums_add_up(bbm):
         l = fit.SampledLoss(fitted, reference, 0, lin)
         b, e = fit.shard_range(lin.size(), r, 4)
         l.begin, l.n = b, e - b
+        l.pairs = lin.directions(b, e - b)
         l.ref = fit.reference_table(reference, lin, b, e - b)
         parts.append(l.probe_sums(fitted._params[None]).cpu().numpy()[0])
     assert abs(sum(parts) - whole) <= 1e-12 * abs(whole)
@@ -196,3 +197,18 @@ def test_compass_on_gpu_follows_reference(bbm, ci):
         assert abs(e - ref_loss[t]) <= 1e-5 * ref_loss[t] + 1e-9
     # identical decisions unless two probes tie within float summation error (then both paths are valid)
     assert same == run["steps"], f"diverged at step {same}"
+
+
+@pytest.mark.parametrize("lin_kind", ["merl", "grid1"])
+def test_materialized_pairs_equal_computed_linearizer(bbm, lin_kind):
+    """bbm_hip_loss_pairs over the materialised pairs == bbm_hip_loss computing the linearizer in-kernel,
+    bit for bit (the pairs come from the same device code)."""
+    from bbm_amd import fit
+    name = "Aggregate<Lambertian,Bagher>"
+    fitted = _model(bbm, name, FIT[f"{name}_fitted"])
+    reference = _model(bbm, name, FIT[f"{name}_reference"])
+    lin = fit.merl_linearizer() if lin_kind == "merl" else _lin(META_FIT["grids"][lin_kind])
+    a = fit.SampledLoss(fitted, reference, "standardLog", lin, materialize=True)
+    b = fit.SampledLoss(fitted, reference, "standardLog", lin, materialize=False)
+    probes = np.stack([fitted._params, reference._params, fitted._params * np.float32(1.01)])
+    np.testing.assert_array_equal(a.probe_sums(probes).cpu().numpy(), b.probe_sums(probes).cpu().numpy())
