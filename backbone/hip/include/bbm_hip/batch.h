@@ -150,8 +150,32 @@ namespace bbm {
         else if constexpr (std::is_same_v<M, bbm::lowashikhminshirley<C>>) return "LowAshikhminShirley";
         else
 #endif
+#ifdef _BBM_BAGHER_H_
+        if constexpr (std::is_same_v<M, bbm::bagher<C>>) return "Bagher";
+        else
+#endif
         static_assert(dependent_false<M>::value, "this bsdfmodel composition has no HIP kernel (see DESIGN.md)");
         return nullptr;
+      }
+
+#ifdef _BBM_AGGREGATEMODEL_H_
+      //! \brief aggregatemodel<lambertian<C>, X> (include/bsdfmodel/aggregatemodel.h:222): the form of every
+      //! published fit; the kernel is registered as "Aggregate<Lambertian,X>"
+      template<typename M> struct lambertian_aggregate : std::false_type {};
+      template<typename C, typename X>
+        struct lambertian_aggregate<bbm::aggregatemodel<bbm::lambertian<C>, X>> : std::true_type { using child = X; };
+#else
+      template<typename M> struct lambertian_aggregate : std::false_type {};
+#endif
+
+      //! \brief Registry name of MODEL's kernel (single models and Aggregate(Lambertian, X))
+      template<typename MODEL>
+        inline std::string registry_name()
+      {
+        using M = std::decay_t<MODEL>;
+        if constexpr (lambertian_aggregate<M>::value)
+          return std::string("Aggregate<Lambertian,") + gpu_name<typename lambertian_aggregate<M>::child>() + ">";
+        else return gpu_name<M>();
       }
     } // end detail namespace
 
@@ -159,7 +183,7 @@ namespace bbm {
     template<typename MODEL>
       inline int model_id()
     {
-      static const int id = [] { int i = bbm_hip_model_id(detail::gpu_name<MODEL>()); check(i); return i; }();
+      static const int id = [] { int i = bbm_hip_model_id(detail::registry_name<MODEL>().c_str()); check(i); return i; }();
       return id;
     }
 
@@ -216,6 +240,37 @@ namespace bbm {
       check(bbm_hip_sample(model_id<MODEL>(), p.data(), int(p.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
                            uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf, flag,
                            stream));
+    }
+
+    //! \brief reflectance of N out directions -> RGB (bsdfmodel::reflectance batched)
+    template<typename MODEL>
+      inline void reflectance(const MODEL& model, soa3 out, size_t n, soa3_out rgb,
+                              bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                              const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      auto p = parameters(model);
+      check(bbm_hip_reflectance(model_id<MODEL>(), p.data(), int(p.size()), out.x, out.y, out.z, mask, n,
+                                uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+    }
+
+    //! \brief Sample losses of include/loss/*.h, for loss_sums
+    enum class loss_t : int { nganL2 = BBM_LOSS_NGAN_L2, lowL2 = BBM_LOSS_LOW_L2, bieronL2 = BBM_LOSS_BIERON_L2,
+                              standardLog = BBM_LOSS_STANDARD_LOG, lowLog = BBM_LOSS_LOW_LOG, bieronLog = BBM_LOSS_BIERON_LOG };
+
+    //! \brief sampledlossfunction<MODEL, reference, loss, linearizer>::operator() (sampledlossfunction.h:62-87)
+    //! for nprobes parameter vectors of MODEL's type at once (device array nprobes x parameters(model).size(),
+    //! e.g. the 2P probes of a compass step), over n materialised pairs with reference values ref:
+    //! sums[p] = sum_i loss(model(probes[p]).eval(in_i, out_i), ref_i) in double (device).  Divide by the
+    //! linearizer size (after summing the shards of all GPUs) for the reference's loss value.
+    template<typename MODEL>
+      inline void loss_sums(const MODEL& model, const float* probes, int nprobes, soa3 in, soa3 out, size_t n,
+                            soa3 ref, loss_t loss, double* sums, void* workspace, size_t workspace_bytes,
+                            bsdf_flag component=bsdf_flag::All, void* stream=nullptr)
+    {
+      const int np = int(parameters(model).size());
+      check(bbm_hip_loss_pairs(model_id<MODEL>(), probes, np, nprobes, n, in.x, in.y, in.z, out.x, out.y, out.z,
+                               ref.x, ref.y, ref.z, int(loss), uint32_t(component), 0u, sums, workspace,
+                               workspace_bytes, stream));
     }
 
   } // end hip namespace

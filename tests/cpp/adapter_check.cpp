@@ -25,6 +25,13 @@
 #include "bsdfmodel/lafortune.h"
 #include "bsdfmodel/ashikhminshirleyfull.h"
 #include "bsdfmodel/lowsmooth.h"
+#include "bsdfmodel/cooktorranceheitz.h"
+#include "bsdfmodel/ggxheitz.h"
+#include "bsdfmodel/phongwalter.h"
+#include "bsdfmodel/ribardiere.h"
+#include "bsdfmodel/bagher.h"
+#include "bsdfmodel/aggregatemodel.h"
+#include "loss/cosine_weighted_log.h"
 #include "bbm_hip/batch.h"
 
 #include <hip/hip_runtime_api.h>
@@ -86,6 +93,18 @@ static bool check_model(const MODEL& model, size_t n, unsigned seed)
   auto SX = download(sx, n), SY = download(sy, n), SZ = download(sz, n), SP = download(spdf, n);
   std::vector<uint32_t> SF(n);
   HIPCHECK(hipMemcpy(SF.data(), sflag.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  // reflectance(out) through the adapter vs the reference's own
+  bbm::hip::reflectance(model, out, n, {r.p, g.p, b.p});
+  HIPCHECK(hipDeviceSynchronize());
+  auto RR = download(r, n), RG = download(g, n), RB = download(b, n);
+  size_t bad_refl = 0;
+  for(size_t i = 0; i < n; ++i)
+  {
+    auto rf = model.reflectance(Vec3d(h[3][i], h[4][i], h[5][i]));
+    const float got[3] = {RR[i], RG[i], RB[i]};
+    for(int k = 0; k < 3; ++k)
+      if(!(got[k] == rf[k] || std::fabs(double(got[k]) - double(rf[k])) <= 1e-5 * std::fabs(double(rf[k])) + 1e-7)) ++bad_refl;
+  }
 
   double peak = 0, ppeak = 0;
   std::vector<float> ce(3 * n), cp(n);
@@ -137,9 +156,72 @@ static bool check_model(const MODEL& model, size_t n, unsigned seed)
     }
     if(!(close(SP[i], float(s.pdf)) || close(SP[i], at_dir))) ++bad;
   }
-  const bool ok = bad == 0 && bad_flag == 0;
-  std::printf("{\"model\": \"%s\", \"n\": %zu, \"violations\": %zu, \"flag_mismatch\": %zu, \"max_rel_err\": %.3e, \"ok\": %s}\n",
-              bbm::toString(model).c_str(), n, bad, bad_flag, worst, ok ? "true" : "false");
+  const bool ok = bad == 0 && bad_flag == 0 && bad_refl == 0;
+  std::printf("{\"model\": \"%s\", \"n\": %zu, \"violations\": %zu, \"flag_mismatch\": %zu, \"reflectance_violations\": %zu, \"max_rel_err\": %.3e, \"ok\": %s}\n",
+              bbm::toString(model).c_str(), n, bad, bad_flag, bad_refl, worst, ok ? "true" : "false");
+  return ok;
+}
+
+// sampledlossfunction through the adapter (bbm::hip::loss_sums: 3 probes in one launch) vs the
+// reference's own standardLog_error summed over the same pairs (double sums, 1e-5)
+template<typename MODEL>
+static bool check_loss(const MODEL& fitted, const MODEL& reference, size_t n, unsigned seed)
+{
+  using Vec3d = typename MODEL::Vec3d;
+  std::mt19937 rng(seed);
+  std::uniform_real_distribution<float> u(0.0f, 1.0f);
+  std::vector<float> h[6];
+  for(auto& v : h) v.resize(n);
+  for(size_t i = 0; i < n; ++i)
+    for(int k = 0; k < 2; ++k)
+    {
+      float z = u(rng), phi = 6.2831853f * u(rng), s = std::sqrt(std::max(1.0f - z * z, 0.0f));
+      h[3 * k + 0][i] = s * std::cos(phi); h[3 * k + 1][i] = s * std::sin(phi); h[3 * k + 2][i] = z;
+    }
+  std::vector<dev_buf> d;
+  d.reserve(6);
+  for(int k = 0; k < 6; ++k) { d.emplace_back(n); upload(d.back(), h[k]); }
+  bbm::hip::soa3 in{d[0].p, d[1].p, d[2].p}, out{d[3].p, d[4].p, d[5].p};
+  dev_buf rr(n), rg(n), rb(n);
+  bbm::hip::eval(reference, in, out, n, {rr.p, rg.p, rb.p});
+  // probes: the fitted parameters, the reference's, and the fitted ones scaled by 1.01
+  std::vector<std::vector<float>> pv = {bbm::hip::parameters(fitted), bbm::hip::parameters(reference), bbm::hip::parameters(fitted)};
+  for(auto& x : pv[2]) x *= 1.01f;
+  const size_t np = pv[0].size();
+  std::vector<float> flat;
+  for(auto& v : pv) flat.insert(flat.end(), v.begin(), v.end());
+  dev_buf probes(flat.size());
+  upload(probes, flat);
+  const size_t wsb = bbm_hip_loss_workspace_size(3);
+  void* ws = nullptr;
+  double* sums = nullptr;
+  HIPCHECK(hipMalloc(&ws, wsb));
+  HIPCHECK(hipMalloc(reinterpret_cast<void**>(&sums), 3 * sizeof(double)));
+  bbm::hip::loss_sums(fitted, probes.p, 3, in, out, n, {rr.p, rg.p, rb.p}, bbm::hip::loss_t::standardLog, sums, ws, wsb);
+  double got[3];
+  HIPCHECK(hipMemcpy(got, sums, sizeof(got), hipMemcpyDeviceToHost));
+  (void)hipFree(ws);
+  (void)hipFree(sums);
+  bbm::standardLog_error<bbm::floatRGB> err;
+  bool ok = true;
+  double worst = 0;
+  for(int p = 0; p < 3; ++p)
+  {
+    MODEL m = fitted;
+    auto pvals = bbm::parameter_values(m, bbm::bsdf_attr(0x1F));
+    for(size_t j = 0; j < np; ++j) pvals[j] = pv[p][j];
+    double want = 0;
+    for(size_t i = 0; i < n; ++i)
+    {
+      Vec3d vin(h[0][i], h[1][i], h[2][i]), vout(h[3][i], h[4][i], h[5][i]);
+      want += double(err(vin, vout, m.eval(vin, vout), reference.eval(vin, vout)));
+    }
+    const double e = std::fabs(got[p] - want);
+    worst = std::max(worst, e / std::max(std::fabs(want), 1e-30));
+    ok &= (p == 1) ? (got[p] == 0.0 && want == 0.0) : (e <= 1e-5 * std::fabs(want));
+  }
+  std::printf("{\"loss\": \"standardLog\", \"model\": \"%s\", \"n\": %zu, \"max_rel_err\": %.3e, \"ok\": %s}\n",
+              bbm::toString(fitted).c_str(), n, worst, ok ? "true" : "false");
   return ok;
 }
 
@@ -170,5 +252,26 @@ int main()
   ok &= check_model(bbm::lowsmooth<bbm::floatRGB>(), n, 15);
   ok &= check_model(bbm::lowmicrofacet<bbm::floatRGB>(), n, 16);
   ok &= check_model(bbm::lowashikhminshirley<bbm::floatRGB>(), n, 17);
+  ok &= check_model(bbm::cooktorranceheitz<bbm::floatRGB>(), n, 18);
+  ok &= check_model(bbm::ggxheitz<bbm::floatRGB>(), n, 19);
+  ok &= check_model(bbm::phongwalter<bbm::floatRGB>(), n, 20);
+  ok &= check_model(bbm::ribardiere<bbm::floatRGB>(), n, 21);
+  ok &= check_model(bbm::ribardiereanisotropic<bbm::floatRGB>(), n, 22);
+  ok &= check_model(bbm::bagher<bbm::floatRGB>(), n, 23);
+  using agg_bagher = bbm::aggregatemodel<bbm::lambertian<bbm::floatRGB>, bbm::bagher<bbm::floatRGB>>;
+  using agg_ct = bbm::aggregatemodel<bbm::lambertian<bbm::floatRGB>, bbm::cooktorrance<bbm::floatRGB>>;
+  ok &= check_model(agg_bagher(), n, 24);
+  ok &= check_model(agg_ct(), n, 25);
+  {
+    // a fit: Aggregate(Lambertian, CookTorrance) against a perturbed reference of the same type
+    agg_ct fitted, reference;
+    auto p = bbm::parameter_values(reference, bbm::bsdf_attr(0x1F));
+    for(auto& x : p) x = float(x) * 1.1f;
+    ok &= check_loss(fitted, reference, 1 << 16, 26);
+    agg_bagher bf, br;
+    auto q = bbm::parameter_values(br, bbm::bsdf_attr(0x1F));
+    for(auto& x : q) x = float(x) * 0.9f;
+    ok &= check_loss(bf, br, 1 << 16, 27);
+  }
   return ok ? 0 : 1;
 }
