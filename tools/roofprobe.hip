@@ -62,6 +62,84 @@ __global__ __launch_bounds__(256) void k_probe(Args a)
   }
 }
 
+// variant 5: float4 copy (1 stream in, 1 out), nontemporal -- the guide's copy calibration
+// variant 6: 6in/4out nontemporal, two quads per lane interleaved per wave (quad t and t + 64 of the
+//            wave's 128-quad tile), all 12 loads issued before any store
+// variant 7: read-only nontemporal, variant 8: write-only nontemporal
+template<int V>
+__global__ __launch_bounds__(256) void k_probe2(Args a)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * 256;
+  if (V == 5)
+  {
+    for (uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x; t < a.n4; t += stride)
+      __builtin_nontemporal_store(__builtin_nontemporal_load(&a.in[0][t]), &a.out[0][t]);
+    return;
+  }
+  if (V == 6)
+  {
+    const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t base = uint64_t(blockIdx.x) * 512 + wave * 128; base < a.n4; base += uint64_t(gridDim.x) * 512)
+    {
+      const uint64_t t0 = base + lane, t1 = base + 64 + lane;
+      f4 v[6][2];
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+      {
+        v[k][0] = __builtin_nontemporal_load(&a.in[k][t0 < a.n4 ? t0 : a.n4 - 1]);
+        v[k][1] = __builtin_nontemporal_load(&a.in[k][t1 < a.n4 ? t1 : a.n4 - 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+      {
+        const uint64_t i = u ? t1 : t0;
+        if (i >= a.n4) continue;
+        f4 s = v[0][u];
+        s.x += v[3][u].x; s.y += v[4][u].y; s.z += v[5][u].z; s.w += v[1][u].w + v[2][u].x;
+        __builtin_nontemporal_store(s, &a.out[0][i]); __builtin_nontemporal_store(v[1][u], &a.out[1][i]);
+        __builtin_nontemporal_store(v[2][u], &a.out[2][i]); __builtin_nontemporal_store(v[4][u], &a.out[3][i]);
+      }
+    }
+    return;
+  }
+  for (uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x; t < a.n4; t += stride)
+  {
+    if (V == 8)
+    {
+      const float f = float(t);
+      __builtin_nontemporal_store(f4{f, f, f, f}, &a.out[0][t]); __builtin_nontemporal_store(f4{f, f, f, f}, &a.out[1][t]);
+      __builtin_nontemporal_store(f4{f, f, f, f}, &a.out[2][t]); __builtin_nontemporal_store(f4{f, f, f, f}, &a.out[3][t]);
+      continue;
+    }
+    f4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = __builtin_nontemporal_load(&a.in[k][t]);
+    f4 s = v[0];
+    s.x += v[3].x; s.y += v[4].y; s.z += v[5].z; s.w += v[1].w + v[2].x;
+    if (s.x == 12345.678f) a.out[0][t] = s;
+  }
+}
+
+// variants 9 / 10: each workgroup streams a contiguous chunk of 16 / 64 consecutive 4 KiB tiles per
+// stream (DRAM row locality), nontemporal; grid = n4 / (256 * tiles)
+template<int TILES>
+__global__ __launch_bounds__(256) void k_probe_chunk(Args a)
+{
+  const uint64_t first = uint64_t(blockIdx.x) * TILES * 256;
+  for (int k2 = 0; k2 < TILES; ++k2)
+  {
+    const uint64_t t = first + uint64_t(k2) * 256 + threadIdx.x;
+    if (t >= a.n4) return;
+    f4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = __builtin_nontemporal_load(&a.in[k][t]);
+    f4 s = v[0];
+    s.x += v[3].x; s.y += v[4].y; s.z += v[5].z; s.w += v[1].w + v[2].x;
+    __builtin_nontemporal_store(s, &a.out[0][t]); __builtin_nontemporal_store(v[1], &a.out[1][t]);
+    __builtin_nontemporal_store(v[2], &a.out[2][t]); __builtin_nontemporal_store(v[4], &a.out[3][t]);
+  }
+}
+
 extern "C" int roofprobe(int variant, const float* const* in, float* const* out, uint64_t n, int blocks, void* stream)
 {
   Args a;
@@ -76,6 +154,13 @@ extern "C" int roofprobe(int variant, const float* const* in, float* const* out,
     case 2: hipLaunchKernelGGL(k_probe<2>, dim3(blocks), dim3(256), 0, s, a); break;
     case 3: hipLaunchKernelGGL(k_probe<3>, dim3(blocks), dim3(256), 0, s, a); break;
     case 4: hipLaunchKernelGGL(k_probe<4>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 5: hipLaunchKernelGGL(k_probe2<5>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 6: hipLaunchKernelGGL(k_probe2<6>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 7: hipLaunchKernelGGL(k_probe2<7>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(k_probe2<8>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 9: hipLaunchKernelGGL(k_probe_chunk<16>, dim3((a.n4 + 16 * 256 - 1) / (16 * 256)), dim3(256), 0, s, a); break;
+    case 10: hipLaunchKernelGGL(k_probe_chunk<64>, dim3((a.n4 + 64 * 256 - 1) / (64 * 256)), dim3(256), 0, s, a); break;
+    case 11: hipLaunchKernelGGL(k_probe_chunk<4>, dim3((a.n4 + 4 * 256 - 1) / (4 * 256)), dim3(256), 0, s, a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
