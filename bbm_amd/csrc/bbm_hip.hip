@@ -28,6 +28,8 @@ BBM_HIP_LOBE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_DIFFUSE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_SPECTRAL_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_AGGREGATE_MODELS(BBM_HIP_EXTERN)
+BBM_HIP_EPD_MODELS(BBM_HIP_EXTERN)
+int epd_table_host(float* out, int capacity);
 
 namespace {
 
@@ -123,6 +125,9 @@ const ModelEntry kSingle[] = {
    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, kEpsF, kEpsF, kEpsF, 0, 0, 0, 0, 0, 0, -1, -1, -1},
    {1, 1, 1, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax, kFMax,
     1, 1, 1, kFMax, kFMax, kFMax, 1, 1, 1, 1, 1, 1}, "sssxxxxxxxxxxxxxxxpppppppppppp"},
+  // EPD (bsdfmodel/holzschuchpacanowski.h:34-42): beta, p (ndf/epd.h:180-182), eta = complex ior (n, k)
+  {"EPD", 4, kFlagSpecular, &launch_eval_pdf<EpdM>, &launch_sample<EpdM>, &launch_reflectance<EpdM>, &launch_loss<EpdM>, &launch_check<EpdM>,
+   {0.003f, 0.2f, 1.3f, 0.0f}, {0.0f, 0.0f, 0.1f, 0.0f}, {0.5f, 5.0f, 5.0f, 10.0f}, "pppp"},
 };
 constexpr int kNumSingle = int(sizeof(kSingle) / sizeof(kSingle[0]));
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
@@ -131,7 +136,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && WardM::kParams == 5 && NganWardM::kParams == 4 &&
               PhongLobe::kParams == 4 && LafortuneM::kParams == 7 && NganLafortuneM::kParams == 6 &&
               ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 && NganASM::kParams == 5 &&
-              LowSmooth::kParams == 6 && Bagher::kParams == 30, "registry nparams must match the compositions");
+              LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4, "registry nparams must match the compositions");
 
 // Aggregate(Lambertian, X) (aggregatemodel.h:22-233): parameters, defaults, bounds and attribute
 // flags are Lambertian's followed by X's; `child` names the registry entry X.
@@ -648,6 +653,11 @@ int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprob
   a.pairs[0] = in_x; a.pairs[1] = in_y; a.pairs[2] = in_z;
   a.pairs[3] = out_x; a.pairs[4] = out_y; a.pairs[5] = out_z;
   return e->loss(a, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_epd_g1_table(float* out, int capacity)
+{
+  return epd_table_host(out, capacity);
 }
 
 size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* d)

@@ -267,6 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_check_final(const double* partial, i
 template<class Model>
 int launch_check(int test, const CheckArgs& a, double* acc, hipStream_t s)
 {
+  if (const int rc = host_prepare<Model>::run(s)) return rc;
   const uint32_t bx = check_blocks(a.n, a.nslots);
   const dim3 grid(bx, unsigned(a.nslots));
   switch (test)

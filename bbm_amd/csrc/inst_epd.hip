@@ -1,0 +1,187 @@
+// bbm_amd/csrc/inst_epd.hip -- the EPD model (epd.hpp): kernel instantiations and the on-device
+// construction of its G1 shadowing table, a restatement of the reference's table generator
+// precompute/HolzschuchPacanowski/G1.cpp (the reference's table itself is not copied).
+//
+//   G1(p, t) = 1 / (1 + Delta_j),  p = 5 / (row + 1), t = beta tan(theta) = 1 / conv(x_j), x_j = (j + 1) / 1000
+//   Delta_j  = ((Delta_{j-1} + P_{j-1}) t_j / t_{j-1} - P_{j-1}) + (r_j t_j - 1) P2(r_j, p) dr_j   (G1.cpp:190-215)
+//   P2(r, p) = 2 N sum_i dq_i exp(-(r^2 + q_i^2)^p)   over the 10 000 midpoint intervals   (G1.cpp:91-113)
+//   conv(x)  = log(1/x)^20 (the exponentiated-log encoding of the integration variable)
+//
+// The p- and r-independent pieces (the q_i, dq_i of the P2 loop, the r_j, dr_j, t_j of the series, N per
+// row) are evaluated on the host with the C library's float/double functions and the generator's exact
+// float/double expression types; the 100 x 999 P2 integrals (1e9 terms) run on the GPU, one thread per
+// (row, j) summing its 10 000 terms serially in float like the generator; the recurrence, G1 = 1/(1+Delta)
+// and the rounding to 6 significant digits (the generator prints with bbm::toString, i.e. ostream <<
+// float) are host work again.  Built once per device, on first use of an EPD model.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "kernels.hpp"
+#include "models.hpp"
+
+namespace bbmhip {
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_epd_p2(const float* __restrict__ dq, const float* __restrict__ q, int nq,
+                                                 const float* __restrict__ rj, const float* __restrict__ prow,
+                                                 const float* __restrict__ norm, float* __restrict__ out)
+{
+  const int row = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;    // 1 .. 998 carry a finite tan(theta)
+  if (j < 1 || j >= kEpdCols) return;
+  const float r = rj[j];
+  const float p = prow[row];
+  const float r2 = r * r;
+  float integral = 0.0f;
+  for (int i = 0; i < nq; ++i)
+  {
+    const float qi = q[i];
+    integral += dq[i] * expf(-powf(r2 + qi * qi, p));
+  }
+  out[row * kEpdCols + j] = float(2.0 * double(norm[row]) * double(integral));
+}
+
+struct EpdTable
+{
+  float* dev = nullptr;
+  std::vector<float> host;
+};
+
+std::mutex g_epd_mutex;
+std::map<int, EpdTable> g_epd_tables;      // per device
+
+int hip_fail(hipError_t e, const char* what)
+{
+  return fail(BBM_HIP_ERR_HIP, std::string("EPD G1 table: ") + what + ": " + hipGetErrorString(e));
+}
+
+// conv(x) = pow(log(rcp(x)), gamma) with gamma = Value(20) (G1.cpp:98, :180): float x -> float ops
+// (std::pow(float, float)); double x -> double ops
+float conv_f(float x) { return std::pow(std::log(1.0f / x), 20.0f); }
+double conv_d(double x) { return std::pow(std::log(1.0 / x), double(20.0f)); }
+
+int build_table(hipStream_t s, EpdTable& t)
+{
+  // P2's midpoint loop (G1.cpp:101-108): for(Value x=1; x > deltax; x -= deltax), deltax = Value(0.0001)
+  std::vector<float> dq, q;
+  const float deltax = 0.0001f;
+  for (float x = 1; x > deltax; x -= deltax)
+  {
+    const float d = conv_f(x - deltax) - conv_f(x);
+    const float qq = float(conv_d(double(x) - 0.5 * double(deltax)));
+    if (!std::isnan(d)) { dq.push_back(d); q.push_back(qq); }
+  }
+  // series samples (G1.cpp:190-201)
+  const float delta_x = 1.0f / float(kEpdCols);
+  std::vector<float> tan_t(kEpdCols, 0.0f), dr(kEpdCols, 0.0f), rj(kEpdCols, 0.0f);
+  for (int j = 1; j < kEpdCols; ++j)
+  {
+    const float x = float(j + 1) / float(kEpdCols);
+    tan_t[j] = 1.0f / conv_f(x);
+    dr[j] = conv_f(x - delta_x) - conv_f(x);
+    rj[j] = float(conv_d(double(x) - 0.5 * double(delta_x)));
+  }
+  // rows: p = 5.0 / Value(p_idx + 1) (G1.cpp:282), N = p / (Pi() * tgamma(1.0 / p)) (:93)
+  std::vector<float> prow(kEpdRows), norm(kEpdRows);
+  for (int r = 0; r < kEpdRows; ++r)
+  {
+    prow[r] = float(5.0 / double(float(r + 1)));
+    norm[r] = float(double(prow[r]) / (double(kPiF) * std::tgamma(1.0 / double(prow[r]))));
+  }
+
+  const size_t nq = dq.size();
+  float *d_dq = nullptr, *d_q = nullptr, *d_r = nullptr, *d_p = nullptr, *d_n = nullptr, *d_out = nullptr;
+  hipError_t e;
+  if ((e = hipMalloc(&d_dq, nq * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMalloc(&d_q, nq * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMalloc(&d_r, kEpdCols * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMalloc(&d_p, kEpdRows * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMalloc(&d_n, kEpdRows * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMalloc(&d_out, size_t(kEpdRows) * kEpdCols * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  hipMemcpyAsync(d_dq, dq.data(), nq * 4, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_q, q.data(), nq * 4, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_r, rj.data(), kEpdCols * 4, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_p, prow.data(), kEpdRows * 4, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_n, norm.data(), kEpdRows * 4, hipMemcpyHostToDevice, s);
+  hipLaunchKernelGGL(k_epd_p2, dim3((kEpdCols + 255) / 256, kEpdRows), dim3(256), 0, s, d_dq, d_q, int(nq), d_r, d_p,
+                     d_n, d_out);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "kernel launch");
+  std::vector<float> p2(size_t(kEpdRows) * kEpdCols);
+  hipMemcpyAsync(p2.data(), d_out, p2.size() * 4, hipMemcpyDeviceToHost, s);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "synchronize");
+  hipFree(d_dq); hipFree(d_q); hipFree(d_r); hipFree(d_p); hipFree(d_n); hipFree(d_out);
+
+  // the Delta recurrence and G1 = 1 / (1 + Delta) per row (G1.cpp:186-220), then the 6-digit print
+  t.host.assign(size_t(kEpdRows) * kEpdCols, 0.0f);
+  for (int r = 0; r < kEpdRows; ++r)
+  {
+    std::vector<float> integral(kEpdCols, 0.0f);
+    float prev = 0.0f, Pj = 0.0f;
+    for (int j = 1; j < kEpdCols; ++j)
+    {
+      const float tt = tan_t[j];
+      if (!std::isinf(tt))
+      {
+        const float p2j = p2[size_t(r) * kEpdCols + j] * dr[j];
+        float v = 0.0f;
+        if (prev > 0) v = (integral[j - 1] + Pj) * tt / prev - Pj;
+        if (rj[j] * tt > 1) v += (rj[j] * tt - 1) * p2j;
+        integral[j] = v;
+        prev = tt;
+        Pj += p2j;
+      }
+      else integral[j] = tt;
+    }
+    for (int j = 0; j < kEpdCols; ++j)
+    {
+      const float g = float(1.0 / (1.0 + double(integral[j])));
+      char buf[64];
+      std::snprintf(buf, sizeof(buf), "%g", double(g));        // ostream << float, precision 6
+      t.host[size_t(r) * kEpdCols + j] = float(std::strtod(buf, nullptr));   // a double literal in G1.h
+    }
+  }
+  if ((e = hipMalloc(&t.dev, t.host.size() * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
+  if ((e = hipMemcpy(t.dev, t.host.data(), t.host.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return hip_fail(e, "upload");
+  return BBM_HIP_OK;
+}
+
+}  // namespace
+
+int epd_prepare(hipStream_t s)
+{
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lock(g_epd_mutex);
+  auto it = g_epd_tables.find(dev);
+  if (it != g_epd_tables.end()) return BBM_HIP_OK;
+  EpdTable t;
+  const int rc = build_table(s, t);
+  if (rc) return rc;
+  // this unit's g_epd_g1 is the one its kernels read
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_epd_g1), &t.dev, sizeof(t.dev))) != hipSuccess) return hip_fail(e, "set symbol");
+  g_epd_tables.emplace(dev, std::move(t));
+  return BBM_HIP_OK;
+}
+
+// Host copy of the table (tests: compared with the reference's G1.h through the oracle shim).
+int epd_table_host(float* out, int capacity)
+{
+  if (const int rc = epd_prepare(nullptr)) return rc;
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(g_epd_mutex);
+  const auto& h = g_epd_tables[dev].host;
+  for (int i = 0; out && i < capacity && i < int(h.size()); ++i) out[i] = h[size_t(i)];
+  return int(h.size());
+}
+
+BBM_HIP_EPD_MODELS(BBM_HIP_INSTANTIATE)
+
+}  // namespace bbmhip

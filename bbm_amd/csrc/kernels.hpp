@@ -32,6 +32,9 @@ int fail(int code, const std::string& msg);
 
 struct ParamBlock { float v[kMaxParams]; };
 
+// Per-model host work before a launch (e.g. building a lookup table on first use); no-op by default.
+template<class Model> struct host_prepare { static int run(hipStream_t) { return 0; } };
+
 struct EvalArgs
 {
   const float* ix; const float* iy; const float* iz;
@@ -369,6 +372,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 template<class Model, int MODE, bool MASK>
 int launch_mode(const EvalArgs& a, hipStream_t s)
 {
+  if (const int rc = host_prepare<Model>::run(s)) return rc;
   bool vec = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
              aligned16(a.oz) && (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
   if (MODE & kModeEval) vec = vec && aligned16(a.r) && aligned16(a.g) && aligned16(a.b);
@@ -400,6 +404,7 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
 template<class Model, bool MASK>
 int launch_sample_mask(const SampleArgs& a, hipStream_t s)
 {
+  if (const int rc = host_prepare<Model>::run(s)) return rc;
   const bool vec = aligned16(a.ox) && aligned16(a.oy) && aligned16(a.oz) && aligned16(a.xi0) && aligned16(a.xi1) &&
                    aligned16(a.dx) && aligned16(a.dy) && aligned16(a.dz) && aligned16(a.pdf) && aligned16(a.flag) &&
                    (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
@@ -462,6 +467,7 @@ __global__ __launch_bounds__(kBlock) void k_reflectance(ReflArgs a)
 template<class Model>
 int launch_reflectance(const ReflArgs& a, hipStream_t s)
 {
+  if (const int rc = host_prepare<Model>::run(s)) return rc;
   uint64_t blocks = (a.n + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
@@ -552,6 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums,
 template<class Model>
 int launch_loss(const LossArgs& a0, hipStream_t s)
 {
+  if (const int rc = host_prepare<Model>::run(s)) return rc;
   LossArgs a = a0;
   uint64_t blocks = (a.n + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;

@@ -184,7 +184,7 @@ struct Lafortune
       : cx(p[3]), cy(Aniso ? p[4] : p[3]), cz(p[Aniso ? 5 : 4]), s(p[Aniso ? 6 : 5])
   {
     albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2];
-    ngan = NGAN ? (s + 2.0) * kInvPiHalfF / double(powf(fmaxf(cz * cz, cx * cx), s * 0.5f)) : 1.0;
+    ngan = NGAN ? (s + 2.0) * kInvPiHalfF / double(powf_cr(fmaxf(cz * cz, cx * cx), s * 0.5f)) : 1.0;   // glibc powf
   }
 
   template<int MODE>

@@ -7,6 +7,7 @@
 #include "microfacet.hpp"
 #include "spectral.hpp"
 #include "aggregate.hpp"
+#include "epd.hpp"
 
 namespace bbmhip {
 
@@ -60,6 +61,7 @@ using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
   X(ASM) X(ASFullM) X(LowASM) X(NganASM) X(LowSmooth)
 #define BBM_HIP_DIFFUSE_MODELS(X) X(Lambertian) X(OrenNayar)
 #define BBM_HIP_SPECTRAL_MODELS(X) X(Bagher)
+#define BBM_HIP_EPD_MODELS(X) X(EpdM)
 #define BBM_HIP_AGGREGATE_MODELS(X) \
   X(AggBagherM) X(AggCookTorranceM) X(AggGGXM) X(AggLowASM) X(AggLowMicrofacetM) X(AggLowSmoothM) X(AggNganASM) \
   X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM)

@@ -50,6 +50,7 @@ ATTRIBUTES = {
     "LowAshikhminShirley": [("albedo", RGB), ("fresnelReflectance", S), ("sharpness", S)],  # low.h:24-25
     "NganAshikhminShirley": [("albedo", RGB), ("fresnelReflectance", S), ("sharpness", S)],  # ngan.h:157-158
     "LowSmooth": [("A", RGB), ("B", S), ("C", S), ("eta", S)],                             # lowsmooth.h:17-194
+    "EPD": [("beta", S), ("p", S), ("eta", V2)],            # holzschuchpacanowski.h:34-42, ndf/epd.h:180-182; eta = (n, k)
 }
 
 

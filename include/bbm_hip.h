@@ -181,6 +181,12 @@ int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprob
                        int loss_kind, uint32_t component, uint32_t unit,
                        double* sums, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The EPD model's shadowing table G1[p][t] (100 x 1000 floats, row-major; the reference's
+ * include/precomputed/holzschuchpacanowski/G1.h), built on the current device on first use by
+ * restating its generator (precompute/HolzschuchPacanowski/G1.cpp).  Copies min(capacity, 100000)
+ * entries to host memory `out` (may be NULL) and returns the table size, or a negative error code. */
+int bbm_hip_epd_g1_table(float* out, int capacity);
+
 /* ---------------------------------------------------------------- synthetic directions */
 
 /* Fill n directions from a counter-based generator: element i depends only on (seed, offset + i),

@@ -73,3 +73,14 @@ void bbmref_chi2_bin_points(size_t n, const uint32_t* t, const uint32_t* p, cons
 double bbmref_gamma_q(float a, float x) { return double(bbm::gamma_q(a, x)); }
 
 } // extern "C"
+
+extern "C" {
+/* The reference's precomputed EPD shadowing table (include/precomputed/holzschuchpacanowski/G1.h), row-major
+ * [p][t] -- compared entry by entry with the table libbbm_hip builds on the GPU. */
+int bbmref_epd_g1(float* out, int cap)
+{
+  const auto& t = bbm::precomputed::holzschuchpacanowski::G1;
+  for(size_t i=0; out && i < t.size() && int(i) < cap; ++i) out[i] = t[i];
+  return int(t.size());
+}
+} // extern "C"

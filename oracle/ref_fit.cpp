@@ -284,6 +284,7 @@ const std::vector<std::pair<const char*, std::vector<uint32_t> (*)()>>& attr_reg
     BBMREF_ATTRS(phong), BBMREF_ATTRS(nganblinnphong), BBMREF_ATTRS(lafortune), BBMREF_ATTRS(nganlafortune),
     BBMREF_ATTRS(ashikhminshirley), BBMREF_ATTRS(ashikhminshirleyfull), BBMREF_ATTRS(lowashikhminshirley),
     BBMREF_ATTRS(nganashikhminshirley), BBMREF_ATTRS(lowsmooth),
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "EPD", &param_attrs<bbmref::epd<C>> },
   };
   return r;
 }

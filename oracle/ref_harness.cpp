@@ -61,6 +61,7 @@ const std::vector<entry>& registry()
     BBMREF_ENTRY(lowashikhminshirley),
     BBMREF_ENTRY(nganashikhminshirley),
     BBMREF_ENTRY(lowsmooth),
+    BBMREF_ENTRY_NS(bbmref, epd),
   };
   return r;
 }
