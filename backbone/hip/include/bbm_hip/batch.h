@@ -154,6 +154,10 @@ namespace bbm {
         if constexpr (std::is_same_v<M, bbm::bagher<C>>) return "Bagher";
         else
 #endif
+#ifdef _BBM_HOLZSCHUCHPACANOWSKI_H_
+        if constexpr (std::is_same_v<M, bbm::epd<C>>) return "EPD";
+        else
+#endif
         static_assert(dependent_false<M>::value, "this bsdfmodel composition has no HIP kernel (see DESIGN.md)");
         return nullptr;
       }
