@@ -29,6 +29,7 @@ BBM_HIP_DIFFUSE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_SPECTRAL_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_AGGREGATE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_EPD_MODELS(BBM_HIP_EXTERN)
+BBM_HIP_HE_MODELS(BBM_HIP_EXTERN)
 int epd_table_host(float* out, int capacity);
 
 namespace {
@@ -128,6 +129,17 @@ const ModelEntry kSingle[] = {
   // EPD (bsdfmodel/holzschuchpacanowski.h:34-42): beta, p (ndf/epd.h:180-182), eta = complex ior (n, k)
   {"EPD", 4, kFlagSpecular, &launch_eval_pdf<EpdM>, &launch_sample<EpdM>, &launch_reflectance<EpdM>, &launch_loss<EpdM>, &launch_check<EpdM>,
    {0.003f, 0.2f, 1.3f, 0.0f}, {0.0f, 0.0f, 0.1f, 0.0f}, {0.5f, 5.0f, 5.0f, 10.0f}, "pppp"},
+  // He family (bsdfmodel/he.h:473-477, :489-496; ngan.h:166-167): roughness, autocorrelation, eta (complex RGB:
+  // n RGB, k RGB; NganHe: albedo first and a scalar ior)
+#define BBM_HIP_HE_ENTRY(NAME, M)                                                                             \
+  {NAME, 8, kFlagSpecular, &launch_eval_pdf<M>, &launch_sample<M>, &launch_reflectance<M>, &launch_loss<M>, &launch_check<M>, \
+   {0.18f, 3.0f, 1.3f, 1.3f, 1.3f, 0, 0, 0}, {0, 0, 0.1f, 0.1f, 0.1f, 0, 0, 0},                                 \
+   {kFMax, kFMax, 5, 5, 5, 10, 10, 10}, "pppppppp"}
+  BBM_HIP_HE_ENTRY("He", HeM),
+  BBM_HIP_HE_ENTRY("HeWestin", HeWestinM),
+  BBM_HIP_HE_ENTRY("HeHolzschuch", HeHolzschuchM),
+  {"NganHe", 6, kFlagSpecular, &launch_eval_pdf<NganHeM>, &launch_sample<NganHeM>, &launch_reflectance<NganHeM>, &launch_loss<NganHeM>, &launch_check<NganHeM>,
+   {0.5f, 0.5f, 0.5f, 0.18f, 3.0f, 1.3f}, {0, 0, 0, 0, 0, 1}, {1, 1, 1, kFMax, kFMax, 5}, "sssppp"},
 };
 constexpr int kNumSingle = int(sizeof(kSingle) / sizeof(kSingle[0]));
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
@@ -136,7 +148,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && WardM::kParams == 5 && NganWardM::kParams == 4 &&
               PhongLobe::kParams == 4 && LafortuneM::kParams == 7 && NganLafortuneM::kParams == 6 &&
               ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 && NganASM::kParams == 5 &&
-              LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4, "registry nparams must match the compositions");
+              LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4 && HeM::kParams == 8 && NganHeM::kParams == 6, "registry nparams must match the compositions");
 
 // Aggregate(Lambertian, X) (aggregatemodel.h:22-233): parameters, defaults, bounds and attribute
 // flags are Lambertian's followed by X's; `child` names the registry entry X.

@@ -265,9 +265,13 @@ inline uint32_t check_blocks(uint64_t n, int nslots)
 __global__ __launch_bounds__(kBlock) void k_check_final(const double* partial, int nblocks, double* acc);
 
 template<class Model>
-int launch_check(int test, const CheckArgs& a, double* acc, hipStream_t s)
+int launch_check(int test, const CheckArgs& a0, double* acc, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  CheckArgs a = a0;
+  void* scratch = nullptr;
+  if (const int rc = host_params<Model>::run(a.p, kFlagAll, s, &scratch)) return rc;
+  struct Release { void* p; hipStream_t s; ~Release() { host_params<Model>::done(p, s); } } release{scratch, s};
   const uint32_t bx = check_blocks(a.n, a.nslots);
   const dim3 grid(bx, unsigned(a.nslots));
   switch (test)

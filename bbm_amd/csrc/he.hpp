@@ -1,0 +1,375 @@
+// bbm_amd/csrc/he.hpp -- He et al. 1991's physically based BSDF (include/bsdfmodel/he.h:115-482) with
+// BBM's data-driven importance sampler (include/bbm/ndf_sampler.h, include/ndf/sampler.h):
+//
+//   He           = ndf_sampler< he_base< complex Fresnel (RGB), WithoutExp, Regular, 4 NR steps, 64 Taylor, adaptive, 18 > >
+//   HeWestin     = ndf_sampler< he_base< complex Fresnel (RGB), Errata,     Westin,  4, 64, adaptive, 18 > >
+//   HeHolzschuch = ndf_sampler< he_base< complex Fresnel (RGB), Errata,     Regular, 4, 10, fixed,   none > >
+//   NganHe       = scaledmodel< ndf_sampler< he_base< cook Fresnel (scalar), Errata, Westin, 4, 64, adaptive, 18 > > >
+//                  (include/bsdfmodel/he.h:489-496, ngan.h:166-167)
+//
+// eval = the He model term by term (shadowing S, geometry G, the Taylor-series distribution D, Fresnel);
+// sample / pdf use a 90-bin CDF over theta_h of the model's own backscatter eval(h, h) (ndf/sampler.h:143-181).
+// That CDF depends on the parameters and the sampled component, so it is built per launch on the GPU
+// (k_he_cdf: 90 evaluations + the serial float prefix sum of util/cdf.h:39-47) into stream-ordered
+// scratch memory whose address travels in the parameter block after the model's parameters; the kernels
+// read it from there (host_params<He<...>> below).  No host synchronisation.
+#pragma once
+#include "math.hpp"
+#include "microfacet.hpp"
+#include "fit.hpp"       // theta_of, sph_to_vec, cossin_cr
+#include "kernels.hpp"   // host_params, ParamBlock
+
+namespace bbmhip {
+
+constexpr int kHeBins = 90;                                      // samplesTheta (he.h:490)
+constexpr float kPiHalfF = float(0.5 * kPiD);                    // Constants::Pi(0.5)
+constexpr float kPiSqQuarterF = (0.25f * kPiF) * kPiF;           // Constants::Pi2(0.25) = scale * Pi() * Pi() in float
+constexpr float kPiSqFourF = (4.0f * kPiF) * kPiF;               // Constants::Pi2(4)
+// floatRGB::wavelength() (backbone/native/include/backbone.h:36), in micron
+constexpr float kWavelength[3] = {float(0.645), float(0.526), float(0.444)};
+
+// the CDF pointer rides in two parameter slots (bit pattern of a 64-bit address)
+__host__ __device__ __forceinline__ const float* param_ptr(const float* p, int slot)
+{
+  uint32_t lo, hi;
+  __builtin_memcpy(&lo, p + slot, 4);
+  __builtin_memcpy(&hi, p + slot + 1, 4);
+  return reinterpret_cast<const float*>((uint64_t(hi) << 32) | lo);
+}
+inline void set_param_ptr(float* p, int slot, const void* ptr)
+{
+  const uint64_t v = reinterpret_cast<uint64_t>(ptr);
+  const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  __builtin_memcpy(p + slot, &lo, 4);
+  __builtin_memcpy(p + slot + 1, &hi, 4);
+}
+
+// std::lerp for floats (libstdc++ <cmath>)
+__device__ __forceinline__ float std_lerpf(float a, float b, float t)
+{
+  if ((a <= 0 && b >= 0) || (a >= 0 && b <= 0)) return t * b + (1 - t) * a;
+  if (t == 1) return b;
+  const float x = a + t * (b - a);
+  return ((t > 1) == (b > a)) ? ((b < x) ? x : b) : ((x < b) ? x : b);
+}
+
+// fresnel::complex<CONF, Spectrum> per channel (include/bbm/fresnel_complex.h:38-63); params = n RGB, k RGB
+struct FresnelComplexRGB
+{
+  static constexpr int kParams = 6;
+  float n[3], k[3];
+  __device__ explicit FresnelComplexRGB(const float* q)
+  {
+    for (int c = 0; c < 3; ++c) { n[c] = q[c]; k[c] = q[3 + c]; }
+  }
+  __device__ __forceinline__ void eval3(float cs, float* F) const
+  {
+    const float c2 = cs * cs;
+    const float s2 = 1 - c2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      const float n2 = n[c] * n[c], k2 = k[c] * k[c];
+      const float temp = n2 - k2 - s2;
+      const float a2b2 = safe_sqrtf(temp * temp + 4 * n2 * k2);
+      const double a = safe_sqrt(0.5 * double(a2b2 + temp));
+      const double a2c = 2 * a * double(cs);
+      const double Rs = (double(a2b2) - a2c + double(c2)) / (double(a2b2) + a2c + double(c2));
+      const double ca = double(c2 * a2b2);
+      const double Rp = Rs * (ca - (a2c - double(s2)) * double(s2)) / (ca + (a2c + double(s2)) * double(s2));
+      F[c] = float(0.5 * (Rs + Rp));
+    }
+  }
+};
+
+// fresnel::cook with a scalar ior, broadcast to RGB (NganHe)
+struct FresnelCookRGB
+{
+  static constexpr int kParams = 1;
+  FresnelCook f;
+  __device__ explicit FresnelCookRGB(const float* q) : f(q) {}
+  __device__ __forceinline__ void eval3(float cs, float* F) const { F[0] = F[1] = F[2] = f.eval(cs); }
+};
+
+// EQ25 errata, EQ78 Westin, Taylor terms, adaptive stop, rough approximation threshold (< 0: none), scaled
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct He
+{
+  static constexpr int kOff = SCALED ? 3 : 0;
+  static constexpr int kParams = kOff + 2 + FRES::kParams;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  float albedo[3];
+  float sigma0, tau;
+  FRES fres;
+  const float* cdf;      // kHeBins floats (the launch's component); only valid where host_params ran
+
+  __device__ explicit He(const float* p) : sigma0(p[kOff]), tau(p[kOff + 1]), fres(p + kOff + 2)
+  {
+    for (int c = 0; c < 3; ++c) albedo[c] = SCALED ? p[c] : 1.0f;
+    cdf = param_ptr(p, kParams);
+  }
+
+  // S1 (he.h:266-291), Eqs. 24-25
+  __device__ __forceinline__ float S1(v3 v) const
+  {
+    const bool smooth = sigma0 < kEpsF;
+    const float cot = div_nr(1.0f, tan_theta(v));
+    const float scot = float(double(tau * cot) / (2.0 * double(sigma0)));
+    const float erfc_ = float(0.5 * double(erfcf(scot)));
+    float lambda = float(0.5 * double(kInvSqrtPiF) / double(scot));
+    if (ERRATA) lambda = float(double(lambda) * exp(-(double(scot) * double(scot))));
+    lambda -= erfc_;
+    const float S = float((1.0 - double(erfc_)) / (double(lambda) + 1.0));
+    return smooth ? 1.0f : S;
+  }
+
+  // G (he.h:306-352), Eq. 76
+  __device__ __forceinline__ float G(v3 in, v3 out) const
+  {
+    const v3 v = mk3(in.x + out.x, in.y + out.y, in.z + out.z);
+    const float vq = div_nr(dot3(v, v), v.z);
+    const float v_scale = float(double(vq) * double(vq));
+    const float kixn2 = 1 - in.z * in.z;
+    const float krxn2 = 1 - out.z * out.z;
+    const float kikr = dot3(neg3(in), out);
+    const float sikr = out.y * in.x - out.x * in.y;
+    const float srki = in.y * out.x - in.x * out.y;
+    const float pikr = out.z + kikr * in.z;
+    const float prki = in.z + kikr * out.z;
+    const double dd = 1.0 - double(kikr * kikr);
+    const float denom = float(dd * dd);
+    const float nom = float((double(sikr) * double(sikr) + double(pikr) * double(pikr)) *
+                            (double(srki) * double(srki) + double(prki) * double(prki)) / double(krxn2 * kixn2));
+    const float g = div_nr(v_scale * nom, denom);
+    return (denom > kEpsF) ? g : 1.0f;
+  }
+
+  // sigma (he.h:365-400), Eq. 80 by 4 Newton-Raphson steps
+  __device__ __forceinline__ float sigma(v3 in, v3 out) const
+  {
+    const float ti = tan_theta(in), to = tan_theta(out);
+    auto K = [&](float t) { return t * erfcf(div_nr(tau, 2 * sigma0 * t)); };
+    const float Ki = (ti > kEpsF) ? K(ti) : 0.0f;
+    const float Ko = (to > kEpsF) ? K(to) : 0.0f;
+    const float f0 = div_nr(1.0f, sqrtf(kPi8F)) * (Ki + Ko);
+    float x = (f0 <= 1.0f) ? f0 : float(safe_sqrt(2.0 * double(logf_cr(f0))));
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+    {
+      const float expn = float(exp(0.5 * double(x) * double(x)));
+      const float ev = x * expn - f0;
+      const float grad = (1 + x * x) * expn;
+      x -= (grad > kEpsF) ? div_nr(ev, grad) : 0.0f;
+    }
+    const float r = div_nr(sigma0, safe_sqrtf(1 + x * x));
+    return (sigma0 > kEpsF) ? r : 0.0f;
+  }
+
+  // D (he.h:411-467), Eqs. 78-79: Taylor series in g with Beckmann's rough approximation blended in
+  __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
+  {
+    const float vxy2 = sqnorm2(in.x + out.x, in.y + out.y);
+    const float sg = sigma(in, out);
+    double g[3], norm[3];
+    float eb[3];
+    const float tau2 = float(double(tau) * double(tau));
+    const float base = (vxy2 * tau2) / 4.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      const float gg = div_nr((kPi2F * sg) * (in.z + out.z), kWavelength[c]);
+      g[c] = double(gg) * double(gg);
+      const double l2 = double(kWavelength[c]) * double(kWavelength[c]);
+      norm[c] = double(kPiSqQuarterF * tau2) / l2;
+      eb[c] = WESTIN ? float(double(base) * (double(kPiSqFourF) / l2)) : base;
+    }
+    const double gmin = fmin(fmin(g[0], g[1]), g[2]);
+    float rough[3] = {0.0f, 0.0f, 0.0f}, weight = 0.0f;
+    if (APPROX >= 0 && gmin > double(APPROX))
+    {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) rough[c] = float(exp(-double(eb[c]) / g[c]) / g[c]);
+      weight = float(fmin(fmax(gmin - double(APPROX), 0.0), 1.0));
+    }
+    float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
+    bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
+    for (int m = 1; m <= TAYLOR && !converged; ++m)
+    {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+      {
+        last[c] = term[c];
+        gm[c] = float(double(gm[c]) * (g[c] / double(m)));
+        term[c] = float(exp(-g[c] - double(eb[c] / float(m))) * double(gm[c]) / double(m));
+        sum[c] += term[c];
+      }
+      if (ADAPTIVE)
+      {
+        const float tmin = fminf(fminf(term[0], term[1]), term[2]);
+        const float lmin = fminf(fminf(last[0], last[1]), last[2]);
+        converged = (tmin < kEpsF) && (tmin < lmin);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], rough[c], weight)));
+  }
+
+  // he_base::eval (he.h:142-166), x albedo when scaled (scaledmodel.h:50-53)
+  __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    float Dv[3], F[3];
+    const float S = S1(in) * S1(out);
+    const float Gv = G(in, out);
+    D(in, out, Dv);
+    const float cth = float(safe_sqrt(double(1 + dot3(in, out)) / 2.0));
+    fres.eval3(cth, F);
+    const float nrm = div_nr(1.0f, (kPiF * in.z) * out.z);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      float v = (((nrm * F[c]) * S) * Gv) * Dv[c];
+      if (SCALED) v *= albedo[c];
+      rgb[c] = active ? v : 0.0f;
+    }
+  }
+
+  // ndf::sampler::pdf (ndf/sampler.h:102-128) of the halfway vector m
+  __device__ __forceinline__ float sampler_pdf(v3 m) const
+  {
+    const float theta = theta_of(m);
+    const float ti = float(double(sqrtf(theta / kPiHalfF) * float(kHeBins)) - 0.5);
+    const float w = ti - floorf(ti);
+    const float fl = floorf(ti), ce = ceilf(ti);
+    // clamp(cast<Size_t>(floor(ti)), 0, 89): a negative float cast to size_t wraps on x86-64 (-> 89)
+    const int lidx = (fl < 0) ? kHeBins - 1 : min(int(fl), kHeBins - 1);
+    const int uidx = (ce < 0) ? kHeBins - 1 : min(int(ce), kHeBins - 1);
+    auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0f); };
+    const float p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
+    float st, ct;
+    cossin_cr(theta, ct, st);
+    const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * fabsf(st)) * kPi2F;
+    return ((m.z > 0) && (jac > kEpsF)) ? div_nr(p, jac) : 0.0f;
+  }
+
+  template<int MODE>
+  __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
+  {
+    if (MODE & kModeEval) eval_rgb(in, out, component, rgb);
+    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    if (MODE & kModePdf)
+    {
+      // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156): sampler pdf of h / |4 out.h|, z(in), z(out) > 0
+      const bool active = (out.z > 0) && (in.z > 0);
+      const v3 h = halfway(in, out);
+      const float p = float(double(sampler_pdf(h)) / fabs(4.0 * double(dot3(out, h))));
+      pdf = active ? p : 0.0f;
+    }
+    else pdf = 0.0f;
+  }
+
+  // he_base::reflectance (he.h:230-244): Fresnel at z(out) / Pi * 4.0, x albedo when scaled
+  __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    float F[3];
+    fres.eval3(out.z, F);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      float v = float(double(F[c] / kPiF) * 4.0);
+      if (SCALED) v *= albedo[c];
+      rgb[c] = m ? v : 0.0f;
+    }
+  }
+
+  // ndf_sampler::sample (bbm/ndf_sampler.h:78-111) with ndf::sampler::sample (ndf/sampler.h:63-92)
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1) && (out.z > 0))) return;
+    // cdf::sample (util/cdf.h:73-83): lower_bound of xi0, residual within the bin
+    int idx = 0;
+    while (idx < kHeBins && cdf[idx] < xi0) ++idx;
+    const bool valid = idx < kHeBins;
+    const float ev = valid ? cdf[idx] : 0.0f;
+    const float prev = (valid && idx >= 1) ? cdf[idx - 1] : 0.0f;
+    const float cp = ev - prev;
+    const float residual = valid ? (xi0 - prev) / cp : 0.0f;
+    const double xr = fabs(double(residual) - 0.5);
+    const double off = 1 - safe_sqrt(1 - 2 * xr);
+    const double sgn = copysign(1.0, double(residual) - 0.5);
+    const double q = (double(idx) + 0.5 + sgn * off) / double(kHeBins);
+    float theta = float(q * q * double(kPiHalfF));
+    const float phi = kPi2F * xi1;
+    theta = (theta > kPiHalfF) ? kPiF - theta : theta;
+    const v3 h = sph_to_vec(phi, theta);
+    // reflect(out, h) = h dot(h, out) 2.0 - out (core/vec_transform.h:43-44)
+    const float d = dot3(h, out);
+    dir = mk3(2.0f * (h.x * d) - out.x, 2.0f * (h.y * d) - out.y, 2.0f * (h.z * d) - out.z);
+    float rgb[3];
+    eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
+    flag = component;
+  }
+};
+
+// ndf::sampler::initialize (ndf/sampler.h:143-181) for one component: 90 backscatter evaluations
+// hsum(eval(h, h)) at theta = (i / 90)^2 Pi/2, weighted by sin(theta1) sqrt(theta1), theta1 = ((i+1)/90)^2 Pi/2,
+// then cdf(samples) (util/cdf.h:39-47): serial float prefix sum, normalised by the last entry.
+template<class Model>
+__global__ __launch_bounds__(128) void k_he_cdf(ParamBlock p, uint32_t component, float* __restrict__ cdf)
+{
+  __shared__ float s[kHeBins];
+  const Model m(p.v);
+  const int i = threadIdx.x;
+  if (i < kHeBins)
+  {
+    const float q = float(i) / float(kHeBins);
+    const float theta = float(double(q) * double(q) * double(kPiHalfF));
+    const v3 h = sph_to_vec(0.0f, theta);
+    float rgb[3];
+    m.eval_rgb(h, h, component, rgb);
+    float v = ((0.0f + rgb[0]) + rgb[1]) + rgb[2];
+    const float q1 = float(i + 1) / float(kHeBins);
+    const float theta1 = float(double(q1) * double(q1) * double(kPiHalfF));
+    float st, ct;
+    cossin_cr(theta1, ct, st);
+    v *= st * sqrtf(theta1);
+    s[i] = v;
+  }
+  __syncthreads();
+  if (i == 0)
+  {
+    float acc = 0.0f;
+    for (int k = 0; k < kHeBins; ++k) { acc += s[k]; s[k] = acc; }
+    for (int k = 0; k < kHeBins; ++k) cdf[k] = s[k] / acc;
+  }
+}
+
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
+{
+  using M = He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>;
+  static int run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch)
+  {
+    float* cdf = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&cdf), kHeBins * sizeof(float), s);
+    if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("He sampler CDF: hipMallocAsync: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL((k_he_cdf<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
+    if ((e = hipGetLastError()) != hipSuccess)
+      return fail(BBM_HIP_ERR_HIP, std::string("He sampler CDF: launch: ") + hipGetErrorString(e));
+    set_param_ptr(p.v, M::kParams, cdf);
+    *scratch = cdf;
+    return BBM_HIP_OK;
+  }
+  static void done(void* scratch, hipStream_t s) { if (scratch) (void)hipFreeAsync(scratch, s); }
+};
+
+// he.h:489-496, ngan.h:166-167
+using HeM = He<FresnelComplexRGB, false, false, 64, true, 18, false>;
+using HeWestinM = He<FresnelComplexRGB, true, true, 64, true, 18, false>;
+using HeHolzschuchM = He<FresnelComplexRGB, true, false, 10, false, -1, false>;
+using NganHeM = He<FresnelCookRGB, true, true, 64, true, 18, true>;
+
+}  // namespace bbmhip

@@ -35,6 +35,15 @@ struct ParamBlock { float v[kMaxParams]; };
 // Per-model host work before a launch (e.g. building a lookup table on first use); no-op by default.
 template<class Model> struct host_prepare { static int run(hipStream_t) { return 0; } };
 
+// Per-launch derived data a model's sample / pdf need (e.g. a data-driven sampling CDF), enqueued on the
+// launch stream and passed in the parameter block after the model's own parameters; `done` releases the
+// stream-ordered scratch after the launch.  No-op by default.
+template<class Model> struct host_params
+{
+  static int run(ParamBlock&, uint32_t, hipStream_t, void**) { return 0; }
+  static void done(void*, hipStream_t) {}
+};
+
 struct EvalArgs
 {
   const float* ix; const float* iy; const float* iz;
@@ -370,9 +379,14 @@ __global__ __launch_bounds__(kBlock) void k_sample_v1(SampleArgs a)
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 template<class Model, int MODE, bool MASK>
-int launch_mode(const EvalArgs& a, hipStream_t s)
+int launch_mode(const EvalArgs& a0, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  EvalArgs a = a0;
+  void* scratch = nullptr;
+  if (MODE & kModePdf)
+    if (const int rc = host_params<Model>::run(a.p, a.component, s, &scratch)) return rc;
+  struct Release { void* p; hipStream_t s; ~Release() { host_params<Model>::done(p, s); } } release{scratch, s};
   bool vec = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
              aligned16(a.oz) && (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);
   if (MODE & kModeEval) vec = vec && aligned16(a.r) && aligned16(a.g) && aligned16(a.b);
@@ -402,9 +416,13 @@ int launch_mode(const EvalArgs& a, hipStream_t s)
 }
 
 template<class Model, bool MASK>
-int launch_sample_mask(const SampleArgs& a, hipStream_t s)
+int launch_sample_mask(const SampleArgs& a0, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  SampleArgs a = a0;
+  void* scratch = nullptr;
+  if (const int rc = host_params<Model>::run(a.p, a.component, s, &scratch)) return rc;
+  struct Release { void* p; hipStream_t s; ~Release() { host_params<Model>::done(p, s); } } release{scratch, s};
   const bool vec = aligned16(a.ox) && aligned16(a.oy) && aligned16(a.oz) && aligned16(a.xi0) && aligned16(a.xi1) &&
                    aligned16(a.dx) && aligned16(a.dy) && aligned16(a.dz) && aligned16(a.pdf) && aligned16(a.flag) &&
                    (!MASK || (reinterpret_cast<uintptr_t>(a.mask) & 3u) == 0);

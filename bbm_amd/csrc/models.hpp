@@ -8,6 +8,7 @@
 #include "spectral.hpp"
 #include "aggregate.hpp"
 #include "epd.hpp"
+#include "he.hpp"
 
 namespace bbmhip {
 
@@ -62,6 +63,7 @@ using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 #define BBM_HIP_DIFFUSE_MODELS(X) X(Lambertian) X(OrenNayar)
 #define BBM_HIP_SPECTRAL_MODELS(X) X(Bagher)
 #define BBM_HIP_EPD_MODELS(X) X(EpdM)
+#define BBM_HIP_HE_MODELS(X) X(HeM) X(HeWestinM) X(HeHolzschuchM) X(NganHeM)
 #define BBM_HIP_AGGREGATE_MODELS(X) \
   X(AggBagherM) X(AggCookTorranceM) X(AggGGXM) X(AggLowASM) X(AggLowMicrofacetM) X(AggLowSmoothM) X(AggNganASM) \
   X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM)

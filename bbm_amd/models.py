@@ -51,6 +51,10 @@ ATTRIBUTES = {
     "NganAshikhminShirley": [("albedo", RGB), ("fresnelReflectance", S), ("sharpness", S)],  # ngan.h:157-158
     "LowSmooth": [("A", RGB), ("B", S), ("C", S), ("eta", S)],                             # lowsmooth.h:17-194
     "EPD": [("beta", S), ("p", S), ("eta", V2)],            # holzschuchpacanowski.h:34-42, ndf/epd.h:180-182; eta = (n, k)
+    "He": [("roughness", S), ("autocorrelation", S), ("eta", CRGB)],                        # he.h:473-477, :489-490
+    "HeWestin": [("roughness", S), ("autocorrelation", S), ("eta", CRGB)],                  # he.h:492-493
+    "HeHolzschuch": [("roughness", S), ("autocorrelation", S), ("eta", CRGB)],              # he.h:495-496
+    "NganHe": [("albedo", RGB), ("roughness", S), ("autocorrelation", S), ("eta", S)],      # ngan.h:166-167
 }
 
 

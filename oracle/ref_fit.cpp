@@ -285,6 +285,10 @@ const std::vector<std::pair<const char*, std::vector<uint32_t> (*)()>>& attr_reg
     BBMREF_ATTRS(ashikhminshirley), BBMREF_ATTRS(ashikhminshirleyfull), BBMREF_ATTRS(lowashikhminshirley),
     BBMREF_ATTRS(nganashikhminshirley), BBMREF_ATTRS(lowsmooth),
     std::pair<const char*, std::vector<uint32_t> (*)()>{ "EPD", &param_attrs<bbmref::epd<C>> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "He", &param_attrs<bbmref::he<C>> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "HeWestin", &param_attrs<bbmref::hewestin<C>> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "HeHolzschuch", &param_attrs<bbmref::heholzschuch<C>> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "NganHe", &param_attrs<bbmref::nganhe<C>> },
   };
   return r;
 }

@@ -62,6 +62,10 @@ const std::vector<entry>& registry()
     BBMREF_ENTRY(nganashikhminshirley),
     BBMREF_ENTRY(lowsmooth),
     BBMREF_ENTRY_NS(bbmref, epd),
+    BBMREF_ENTRY_NS(bbmref, he),
+    BBMREF_ENTRY_NS(bbmref, hewestin),
+    BBMREF_ENTRY_NS(bbmref, heholzschuch),
+    BBMREF_ENTRY_NS(bbmref, nganhe),
   };
   return r;
 }

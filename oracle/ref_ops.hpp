@@ -40,6 +40,7 @@
 #pragma pop_macro("BBM_CHECK_CONCEPT")
 #include "ndf/epd.h"
 #include "maskingshadowing/vanginneken.h"
+#include "ref_he.hpp"
 
 #include <cstdint>
 #include <cstring>
