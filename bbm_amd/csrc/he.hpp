@@ -102,12 +102,18 @@ struct He
   float sigma0, tau;
   FRES fres;
   const float* cdf;      // kHeBins floats (the launch's component); only valid where host_params ran
+  uint32_t launch_component;   // the component the CDF was built for; lanes passing another one are masked
 
   __device__ explicit He(const float* p) : sigma0(p[kOff]), tau(p[kOff + 1]), fres(p + kOff + 2)
   {
     for (int c = 0; c < 3; ++c) albedo[c] = SCALED ? p[c] : 1.0f;
     cdf = param_ptr(p, kParams);
+    __builtin_memcpy(&launch_component, p + kParams + 2, 4);
   }
+
+  // The kernels mask a lane by passing component 0.  A sampler built for a component without the specular
+  // lobe is 0/0 (NaN) in the reference, and so is this one, but a masked lane is select(mask, ., 0) there.
+  __device__ __forceinline__ bool masked(uint32_t component) const { return component != launch_component; }
 
   // S1 (he.h:266-291), Eqs. 24-25
   __device__ __forceinline__ float S1(v3 v) const
@@ -214,7 +220,9 @@ struct He
     for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], rough[c], weight)));
   }
 
-  // he_base::eval (he.h:142-166), x albedo when scaled (scaledmodel.h:50-53)
+  // he_base::eval (he.h:142-166), x albedo when scaled (scaledmodel.h:50-53); the sampler's backscatter
+  // evaluations (k_he_cdf) see the unscaled he_base, which scaledmodel wraps from outside
+  template<bool SCALE = true>
   __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
   {
     const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
@@ -229,7 +237,7 @@ struct He
     for (int c = 0; c < 3; ++c)
     {
       float v = (((nrm * F[c]) * S) * Gv) * Dv[c];
-      if (SCALED) v *= albedo[c];
+      if (SCALED && SCALE) v *= albedo[c];
       rgb[c] = active ? v : 0.0f;
     }
   }
@@ -260,7 +268,7 @@ struct He
     if (MODE & kModePdf)
     {
       // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156): sampler pdf of h / |4 out.h|, z(in), z(out) > 0
-      const bool active = (out.z > 0) && (in.z > 0);
+      const bool active = (out.z > 0) && (in.z > 0) && !masked(component);
       const v3 h = halfway(in, out);
       const float p = float(double(sampler_pdf(h)) / fabs(4.0 * double(dot3(out, h))));
       pdf = active ? p : 0.0f;
@@ -288,7 +296,7 @@ struct He
                                          uint32_t& flag) const
   {
     dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
-    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1) && (out.z > 0))) return;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1) && (out.z > 0)) || masked(component)) return;
     // cdf::sample (util/cdf.h:73-83): lower_bound of xi0, residual within the bin
     int idx = 0;
     while (idx < kHeBins && cdf[idx] < xi0) ++idx;
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(128) void k_he_cdf(ParamBlock p, uint32_t component
     const float theta = float(double(q) * double(q) * double(kPiHalfF));
     const v3 h = sph_to_vec(0.0f, theta);
     float rgb[3];
-    m.eval_rgb(h, h, component, rgb);
+    m.template eval_rgb<false>(h, h, component, rgb);
     float v = ((0.0f + rgb[0]) + rgb[1]) + rgb[2];
     const float q1 = float(i + 1) / float(kHeBins);
     const float theta1 = float(double(q1) * double(q1) * double(kPiHalfF));
@@ -360,6 +368,7 @@ struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
     if ((e = hipGetLastError()) != hipSuccess)
       return fail(BBM_HIP_ERR_HIP, std::string("He sampler CDF: launch: ") + hipGetErrorString(e));
     set_param_ptr(p.v, M::kParams, cdf);
+    __builtin_memcpy(p.v + M::kParams + 2, &component, 4);
     *scratch = cdf;
     return BBM_HIP_OK;
   }

@@ -113,11 +113,17 @@ struct ops
                       uint32_t component, uint32_t unit, int mode,
                       OUT* r, OUT* g, OUT* b, OUT* pdf, int nthreads)
   {
-    const M m = make(p, np);
+    const M m0 = make(p, np);
     const auto comp = bbm::bsdf_flag(component);
     const auto u = bbm::unit_t(unit);
+    // one model copy per thread: data-driven samplers (he_sampled) cache their CDFs in a mutable map
 #ifdef _OPENMP
-    #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    {
+    const M m = m0;
+#ifdef _OPENMP
+    #pragma omp for schedule(static)
 #endif
     for(size_t i = 0; i < n; ++i)
     {
@@ -130,6 +136,7 @@ struct ops
       }
       if(mode & 2) pdf[i] = OUT(m.pdf(in, out, comp, u));
     }
+    }
   }
 
   template<typename OUT>
@@ -139,11 +146,16 @@ struct ops
                      uint32_t component, uint32_t unit,
                      OUT* dx, OUT* dy, OUT* dz, OUT* pdf, uint32_t* flag, int nthreads)
   {
-    const M m = make(p, np);
+    const M m0 = make(p, np);
     const auto comp = bbm::bsdf_flag(component);
     const auto u = bbm::unit_t(unit);
 #ifdef _OPENMP
-    #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    {
+    const M m = m0;
+#ifdef _OPENMP
+    #pragma omp for schedule(static)
 #endif
     for(size_t i = 0; i < n; ++i)
     {
@@ -153,6 +165,7 @@ struct ops
       dx[i] = OUT(s.direction[0]); dy[i] = OUT(s.direction[1]); dz[i] = OUT(s.direction[2]);
       pdf[i] = OUT(s.pdf);
       flag[i] = uint32_t(s.flag);
+    }
     }
   }
 

@@ -242,6 +242,37 @@ def test_errors_raise(bbm):
 
 DIR_TOL_MAX = 1e-3
 
+# The He family samples its halfway vector from a 90-bin tabulated CDF (ndf/sampler.h:63-92, util/cdf.h:73-83)
+# whose within-bin warp is discontinuous at the bin edges (residual 1 of bin k maps to (k + 1.5) / 90, residual
+# 0 of bin k + 1 to (k + 0.5) / 90) and infinitely steep next to them.  The CDF entries are sums of backscatter
+# evaluations that agree with the reference to ~1e-5 relative, so an xi0 that close to an edge may land in the
+# neighbouring bin and move the direction by a bin width.  Such a lane passes when the reference itself, given
+# an xi0 at most FLIP_ULPS float steps away, returns the GPU's direction (to FLIP_DIR_TOL: the warp is steep
+# there); at most FLIP_MAX_FRAC of the lanes may need this.
+TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
+FLIP_ULPS = 1024
+FLIP_DIR_TOL = 1e-4
+FLIP_MAX_FRAC = 1e-3
+
+
+def _far_lanes_explained_by_bin_flips(name, params, dout, xi, got_dir, derr, component=3):
+    """Indices of lanes with a direction error > DIR_TOL_MAX that no nearby xi0 explains."""
+    far = np.nonzero(derr.max(0) > DIR_TOL_MAX)[0]
+    if name not in TABULATED_SAMPLERS or far.size == 0:
+        return far
+    assert far.size <= max(1, FLIP_MAX_FRAC * derr.shape[1]), f"{name}: {far.size} bin-edge lanes"
+    x0 = xi[0, far].astype(np.float32)
+    steps = np.concatenate([-np.arange(1, FLIP_ULPS + 1), np.arange(1, FLIP_ULPS + 1)])
+    # x0 moved by k float steps (k * ulp(x0): exact for the xi0 of [0, 1) away from powers of two)
+    ulp = np.spacing(x0)
+    xs = np.clip(x0[:, None] + steps[None, :].astype(np.float32) * ulp[:, None], 0, 1).astype(np.float32)
+    m = steps.size
+    o = np.ascontiguousarray(np.repeat(dout[:, far], m, axis=1))
+    x = np.ascontiguousarray(np.stack([xs.ravel(), np.repeat(xi[1, far], m)]).astype(np.float32))
+    ref, _ = ou.oracle_sample(name, params, o, x, component=component, nthreads=8)
+    d = np.abs(np.repeat(got_dir[:, far], m, axis=1) - ref[:3]).max(0).reshape(far.size, m)
+    return far[np.nanmin(d, axis=1) > FLIP_DIR_TOL]
+
 
 def _gpu_sample(model, sout, sxi, **kw):
     s = model.sample(_dev(sout), _dev(sxi), **kw)
@@ -271,7 +302,8 @@ def test_sample_matches_reference_golden(bbm):
             ref = g[f"sample{si}"]
             assert np.array_equal(flag.astype(np.uint8), g[f"sflag{si}"]), f"{name}[{si}] flags"
             derr = np.abs(got[:3].astype(np.float64) - ref[:3])
-            assert np.nanmax(derr) <= DIR_TOL_MAX, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
+            far = _far_lanes_explained_by_bin_flips(name, g[f"params{si}"], INP["sout"], INP["sxi"], got[:3], derr)
+            assert far.size == 0, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
             assert np.mean(derr.max(0) > 1e-5) <= 0.005, f"{name}[{si}] too many directions off by > 1e-5"
             # the pdf of a sample is pdf(direction): for a sharp lobe a 1-ulp direction difference
             # moves it by more than 1e-5, so it is checked at the GPU's own direction (reference
@@ -304,7 +336,8 @@ def test_sample_large_batch_vs_oracle(bbm):
         ref, flag = ou.oracle_sample(name, m.parameter_values(), hout, hxi, nthreads=8)
         assert np.array_equal(s.flag.cpu().numpy().astype(np.uint32), flag), name
         derr = np.abs(got[:3].astype(np.float64) - ref[:3])
-        assert np.nanmax(derr) <= DIR_TOL_MAX, name
+        far = _far_lanes_explained_by_bin_flips(name, m.parameter_values(), hout, hxi, got[:3], derr)
+        assert far.size == 0, f"{name}: {far.size} directions off by > {DIR_TOL_MAX}, e.g. lane {far[:3]}"
         assert np.mean(derr.max(0) > 1e-5) <= 0.005, name
         pref = _sample_pdf_ref(got[3], ref[3], flag,
                                _pdf_at_dir(name, m.parameter_values(), got[:3], hout, hxi, s.flag.cpu().numpy()))
