@@ -199,14 +199,43 @@ struct He
     }
     float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
     bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
+    // term = exp(-g - eb/m) g^m / m! / m, evaluated in double by the reference.  Split as exp(-g) (double, once
+    // per channel) x exp(-eb/m) (float argument eb/m exactly as the reference forms it, accurate float exp):
+    // the float-rounded term moves by an ulp or two, the series by ~1e-7 relative, and the loop body loses
+    // its double exp and divisions (the series is 3 x up to 64 terms per pair, the whole cost of this model)
+    double eg[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp(-g[c]);
+    float egf[3], gf[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { egf[c] = float(eg[c]); gf[c] = float(g[c]); }
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
+      const double rm = inv_small(m);
+      const float rmf = float(rm);
+      float ex[3];
+      if (WESTIN)
+      {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ex[c] = expf_neg(-(eb[c] * rmf));
+      }
+      else ex[0] = ex[1] = ex[2] = expf_neg(-(eb[0] * rmf));   // eb is the same for every channel
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
         last[c] = term[c];
-        gm[c] = float(double(gm[c]) * (g[c] / double(m)));
-        term[c] = float(exp(-g[c] - double(eb[c] / float(m))) * double(gm[c]) / double(m));
+        if (APPROX >= 0)
+        {
+          // the series only runs for min(g) <= APPROX + 1, so g <= (APPROX + 1) (0.645 / 0.444)^2 < 45: exp(-g),
+          // g^m / m! and their product stay normal floats and the products need no double
+          gm[c] = gm[c] * (gf[c] * rmf);
+          term[c] = (egf[c] * gm[c]) * (ex[c] * rmf);
+        }
+        else
+        {
+          gm[c] = float(double(gm[c]) * (g[c] * rm));
+          term[c] = float(eg[c] * double(ex[c]) * double(gm[c]) * rm);
+        }
         sum[c] += term[c];
       }
       if (ADAPTIVE)

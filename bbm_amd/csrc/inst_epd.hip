@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "kernels.hpp"
@@ -105,18 +106,18 @@ int build_table(hipStream_t s, EpdTable& t)
   if ((e = hipMalloc(&d_p, kEpdRows * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
   if ((e = hipMalloc(&d_n, kEpdRows * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
   if ((e = hipMalloc(&d_out, size_t(kEpdRows) * kEpdCols * 4)) != hipSuccess) return hip_fail(e, "hipMalloc");
-  hipMemcpyAsync(d_dq, dq.data(), nq * 4, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_q, q.data(), nq * 4, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_r, rj.data(), kEpdCols * 4, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_p, prow.data(), kEpdRows * 4, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_n, norm.data(), kEpdRows * 4, hipMemcpyHostToDevice, s);
+  const std::pair<float*, const std::vector<float>*> uploads[] = {{d_dq, &dq}, {d_q, &q}, {d_r, &rj}, {d_p, &prow}, {d_n, &norm}};
+  for (const auto& u : uploads)
+    if ((e = hipMemcpyAsync(u.first, u.second->data(), u.second->size() * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(e, "upload");
   hipLaunchKernelGGL(k_epd_p2, dim3((kEpdCols + 255) / 256, kEpdRows), dim3(256), 0, s, d_dq, d_q, int(nq), d_r, d_p,
                      d_n, d_out);
   if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "kernel launch");
   std::vector<float> p2(size_t(kEpdRows) * kEpdCols);
-  hipMemcpyAsync(p2.data(), d_out, p2.size() * 4, hipMemcpyDeviceToHost, s);
+  if ((e = hipMemcpyAsync(p2.data(), d_out, p2.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "download");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "synchronize");
-  hipFree(d_dq); hipFree(d_q); hipFree(d_r); hipFree(d_p); hipFree(d_n); hipFree(d_out);
+  for (float* d : {d_dq, d_q, d_r, d_p, d_n, d_out}) (void)hipFree(d);
 
   // the Delta recurrence and G1 = 1 / (1 + Delta) per row (G1.cpp:186-220), then the 6-digit print
   t.host.assign(size_t(kEpdRows) * kEpdCols, 0.0f);
@@ -177,7 +178,7 @@ int epd_table_host(float* out, int capacity)
 {
   if (const int rc = epd_prepare(nullptr)) return rc;
   int dev = 0;
-  hipGetDevice(&dev);
+  if (const hipError_t e = hipGetDevice(&dev); e != hipSuccess) return hip_fail(e, "hipGetDevice");
   std::lock_guard<std::mutex> lock(g_epd_mutex);
   const auto& h = g_epd_tables[dev].host;
   for (int i = 0; out && i < capacity && i < int(h.size()); ++i) out[i] = h[size_t(i)];

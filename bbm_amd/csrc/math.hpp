@@ -67,6 +67,33 @@ __device__ __forceinline__ float div_nr(float n, float d)
   return __builtin_isfinite(q1) ? q1 : q;
 }
 
+// exp(x) for a float x <= 0 to ~1 ulp without the library's range checks: x log2(e) split in a head (rounded
+// product) and tail (its fma residual + x times log2(e)'s own tail), v_exp_f32 of the head, first-order fix-up
+// by the tail.  Results below the normal range flush to zero.
+__device__ __forceinline__ float expf_neg(float x)
+{
+  constexpr float kLog2eHi = 1.44269502162933349609375f;          // float(log2 e)
+  constexpr float kLog2eLo = 1.925963033500011079e-08f;          // log2 e - kLog2eHi
+  constexpr float kLn2 = 0.693147180559945309f;
+  const float t = x * kLog2eHi;
+  const float e = __builtin_fmaf(x, kLog2eHi, -t) + x * kLog2eLo;
+  const float r = __builtin_amdgcn_exp2f(t);
+  return __builtin_fmaf(r, e * kLn2, r);
+}
+
+// 1 / m for the loop counters of the series kernels (m <= 64), a uniform scalar load instead of a division
+__device__ __forceinline__ double inv_small(int m)
+{
+  static constexpr double kInv[65] = {
+      0.0,      1.0 / 1,  1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,  1.0 / 6,  1.0 / 7,  1.0 / 8,  1.0 / 9,  1.0 / 10,
+      1.0 / 11, 1.0 / 12, 1.0 / 13, 1.0 / 14, 1.0 / 15, 1.0 / 16, 1.0 / 17, 1.0 / 18, 1.0 / 19, 1.0 / 20, 1.0 / 21,
+      1.0 / 22, 1.0 / 23, 1.0 / 24, 1.0 / 25, 1.0 / 26, 1.0 / 27, 1.0 / 28, 1.0 / 29, 1.0 / 30, 1.0 / 31, 1.0 / 32,
+      1.0 / 33, 1.0 / 34, 1.0 / 35, 1.0 / 36, 1.0 / 37, 1.0 / 38, 1.0 / 39, 1.0 / 40, 1.0 / 41, 1.0 / 42, 1.0 / 43,
+      1.0 / 44, 1.0 / 45, 1.0 / 46, 1.0 / 47, 1.0 / 48, 1.0 / 49, 1.0 / 50, 1.0 / 51, 1.0 / 52, 1.0 / 53, 1.0 / 54,
+      1.0 / 55, 1.0 / 56, 1.0 / 57, 1.0 / 58, 1.0 / 59, 1.0 / 60, 1.0 / 61, 1.0 / 62, 1.0 / 63, 1.0 / 64};
+  return kInv[m];
+}
+
 __device__ __forceinline__ double ddiv_nr(double n, double d)
 {
   double r = __builtin_amdgcn_rcp(d);
