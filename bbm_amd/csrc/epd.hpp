@@ -228,10 +228,11 @@ struct FresnelComplex
     const float a2b2 = safe_sqrtf(temp * temp + 4 * n2 * k2);
     const double a = safe_sqrt(0.5 * double(a2b2 + temp));          // float sum, then double
     const double a2c = 2 * a * double(c);
-    const double Rs = (double(a2b2) - a2c + double(c2)) / (double(a2b2) + a2c + double(c2));
+    // the quotients only need float accuracy (F = float(0.5 (Rs + Rp)), two positive terms): f_div_d
+    const float Rs = f_div_d(double(a2b2) - a2c + double(c2), double(a2b2) + a2c + double(c2));
     const double ca = double(c2 * a2b2);                               // float product
-    const double Rp = Rs * (ca - (a2c - double(s2)) * double(s2)) / (ca + (a2c + double(s2)) * double(s2));
-    return float(0.5 * (Rs + Rp));
+    const float Rp = f_div_d(double(Rs) * (ca - (a2c - double(s2)) * double(s2)), ca + (a2c + double(s2)) * double(s2));
+    return float(0.5 * (double(Rs) + double(Rp)));
   }
 };
 

@@ -74,10 +74,12 @@ struct FresnelComplexRGB
       const float a2b2 = safe_sqrtf(temp * temp + 4 * n2 * k2);
       const double a = safe_sqrt(0.5 * double(a2b2 + temp));
       const double a2c = 2 * a * double(cs);
-      const double Rs = (double(a2b2) - a2c + double(c2)) / (double(a2b2) + a2c + double(c2));
+      // numerators and denominators in double like the reference (they cancel near n = 1); the quotients
+      // only need float accuracy: F = float(0.5 (Rs + Rp)) of two positive terms
+      const float Rs = f_div_d(double(a2b2) - a2c + double(c2), double(a2b2) + a2c + double(c2));
       const double ca = double(c2 * a2b2);
-      const double Rp = Rs * (ca - (a2c - double(s2)) * double(s2)) / (ca + (a2c + double(s2)) * double(s2));
-      F[c] = float(0.5 * (Rs + Rp));
+      const float Rp = f_div_d(double(Rs) * (ca - (a2c - double(s2)) * double(s2)), ca + (a2c + double(s2)) * double(s2));
+      F[c] = float(0.5 * (double(Rs) + double(Rp)));
     }
   }
 };
@@ -120,12 +122,13 @@ struct He
   {
     const bool smooth = sigma0 < kEpsF;
     const float cot = div_nr(1.0f, tan_theta(v));
-    const float scot = float(double(tau * cot) / (2.0 * double(sigma0)));
-    const float erfc_ = float(0.5 * double(erfcf(scot)));
-    float lambda = float(0.5 * double(kInvSqrtPiF) / double(scot));
-    if (ERRATA) lambda = float(double(lambda) * exp(-(double(scot) * double(scot))));
+    // the double quotients below are stored straight into floats: f_div_d rounds like the reference
+    const float scot = f_div_d(double(tau * cot), 2.0 * double(sigma0));
+    const float erfc_ = 0.5f * erfcf(scot);   // float(0.5 * double(e)): exact
+    float lambda = f_div_d(0.5 * double(kInvSqrtPiF), double(scot));
+    if (ERRATA) lambda = float(double(lambda) * double(exp_d2f(-(double(scot) * double(scot)))));
     lambda -= erfc_;
-    const float S = float((1.0 - double(erfc_)) / (double(lambda) + 1.0));
+    const float S = f_div_d(1.0 - double(erfc_), double(lambda) + 1.0);
     return smooth ? 1.0f : S;
   }
 
@@ -144,8 +147,8 @@ struct He
     const float prki = in.z + kikr * out.z;
     const double dd = 1.0 - double(kikr * kikr);
     const float denom = float(dd * dd);
-    const float nom = float((double(sikr) * double(sikr) + double(pikr) * double(pikr)) *
-                            (double(srki) * double(srki) + double(prki) * double(prki)) / double(krxn2 * kixn2));
+    const float nom = f_div_d((double(sikr) * double(sikr) + double(pikr) * double(pikr)) *
+                                  (double(srki) * double(srki) + double(prki) * double(prki)), double(krxn2 * kixn2));
     const float g = div_nr(v_scale * nom, denom);
     return (denom > kEpsF) ? g : 1.0f;
   }
@@ -162,7 +165,7 @@ struct He
 #pragma unroll
     for (int s = 0; s < 4; ++s)
     {
-      const float expn = float(exp(0.5 * double(x) * double(x)));
+      const float expn = exp_d2f(0.5 * double(x) * double(x));
       const float ev = x * expn - f0;
       const float grad = (1 + x * x) * expn;
       x -= (grad > kEpsF) ? div_nr(ev, grad) : 0.0f;
@@ -186,7 +189,7 @@ struct He
       const float gg = div_nr((kPi2F * sg) * (in.z + out.z), kWavelength[c]);
       g[c] = double(gg) * double(gg);
       const double l2 = double(kWavelength[c]) * double(kWavelength[c]);
-      norm[c] = double(kPiSqQuarterF * tau2) / l2;
+      norm[c] = double(kPiSqQuarterF * tau2) * (1.0 / l2);   // constant reciprocal: within an ulp of the quotient
       eb[c] = WESTIN ? float(double(base) * (double(kPiSqFourF) / l2)) : base;
     }
     const double gmin = fmin(fmin(g[0], g[1]), g[2]);
@@ -194,7 +197,11 @@ struct He
     if (APPROX >= 0 && gmin > double(APPROX))
     {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) rough[c] = float(exp(-double(eb[c]) / g[c]) / g[c]);
+      for (int c = 0; c < 3; ++c)
+      {
+        const double rg = ddiv_nr(1.0, g[c]);    // g > APPROX here
+        rough[c] = float(double(exp_d2f(-double(eb[c]) * rg)) * rg);
+      }
       weight = float(fmin(fmax(gmin - double(APPROX), 0.0), 1.0));
     }
     float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
@@ -204,11 +211,14 @@ struct He
     // the float-rounded term moves by an ulp or two, the series by ~1e-7 relative, and the loop body loses
     // its double exp and divisions (the series is 3 x up to 64 terms per pair, the whole cost of this model)
     double eg[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp(-g[c]);
     float egf[3], gf[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) { egf[c] = float(eg[c]); gf[c] = float(g[c]); }
+    for (int c = 0; c < 3; ++c)
+    {
+      if (APPROX >= 0) egf[c] = converged ? 0.0f : exp_d2f(-g[c]);
+      else eg[c] = exp(-g[c]);
+      gf[c] = float(g[c]);
+    }
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);

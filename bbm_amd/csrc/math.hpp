@@ -81,6 +81,18 @@ __device__ __forceinline__ float expf_neg(float x)
   return __builtin_fmaf(r, e * kLn2, r);
 }
 
+// float(exp(a)) for a double argument, to ~1 ulp of the float result: a log2(e) in double, split into a float
+// head and tail, v_exp_f32 of the head, first-order fix-up by the tail (a handful of f64 ops instead of a full
+// double exp).  +-inf and overflow give inf / 0 like the reference; results below the normal range flush.
+__device__ __forceinline__ float exp_d2f(double a)
+{
+  const double t = a * 1.4426950408889634074;
+  const float th = float(t);
+  const float tl = float(t - double(th));
+  const float r = __builtin_amdgcn_exp2f(th);
+  return __builtin_isinf(th) ? r : __builtin_fmaf(r, tl * 0.693147180559945309f, r);
+}
+
 // 1 / m for the loop counters of the series kernels (m <= 64), a uniform scalar load instead of a division
 __device__ __forceinline__ double inv_small(int m)
 {

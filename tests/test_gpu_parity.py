@@ -127,6 +127,7 @@ def test_every_gpu_model_matches_reference_golden(bbm):
             m = bbm.BsdfModel(name)
             m.set_parameter_values(g[f"params{si}"])
             got = _gpu_evalpdf(m, INP["pin"], INP["pout"])
+            _save(f"golden_{name}_{si}", got)
             worst[f"{name}[{si}]"] = _assert_parity(got, g[f"evalpdf{si}"], f"{name}[{si}]")
     _report("golden", worst)
 
