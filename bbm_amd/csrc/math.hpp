@@ -240,6 +240,15 @@ __device__ __forceinline__ float pow2f(float x) { return x * x; }
 // 1-ulp expf difference is not amplified; the eval kernels keep the full-rate f32 expf.
 __device__ __forceinline__ float expf_cr(float x) { return float(exp(double(x))); }
 __device__ __forceinline__ float logf_cr(float x) { return float(log(double(x))); }
+// x^y for x >= 0, y > 0, rounded from exp(y log x) in f64: the relative error of the f64 result
+// (~|y log x| 2^-52) is far below float resolution, so this is the correctly rounded powf -- what glibc's
+// powf returns -- except within ~2^-25 ulp of a midpoint; a double log + exp instead of the library powf's
+// extended-precision log and special-case handling.  Only for the domain stated (Bagher's G1: x = theta -
+// theta0 > 0, y = k > 0).
+__device__ __forceinline__ float powf_xlog(float x, float y)
+{
+  return (x > 0.0f) ? float(exp(double(y) * log(double(x)))) : 0.0f;
+}
 // x^y for x > 0 on the transcendental unit: exp2(y log2 x), v_log_f32 + v_exp_f32 (each ~1 ulp).
 // Relative error ~ (1 + |y log2 x|) * 2^-23: below 3e-6 wherever the result is a normal float that
 // matters (|y log2 x| < 25), vs ~100 VALU instructions for the library powf.  x <= 0 gives NaN / 0 / inf

@@ -54,7 +54,9 @@ struct Bagher
   {
     // 1 + Lambda (1 - exp(c pow(...))) cancels catastrophically for published fits (fits/bagher_sgd.fit:
     // k ~ 48, c ~ 1e-7 -> g ~ 5e-4 at grazing angles): pow and theta must round like the reference's
-    const float g = 1.0f + Lambda[j] * (1.0f - expf(c[j] * powf(th - theta0[j], k[j])));
+    // (pow rounded from f64 exp(k log d), which is the correctly rounded powf; powf_xlog's domain holds: d > 0 where
+    // the result is used, and the fit bounds keep k > 0)
+    const float g = 1.0f + Lambda[j] * (1.0f - expf(c[j] * powf_xlog(th - theta0[j], k[j])));
     return (th > theta0[j]) ? g : 1.0f;
   }
 
