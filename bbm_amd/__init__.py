@@ -18,8 +18,12 @@ _lib.load()
 __all__ = ["Aggregate", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
            "fill_directions", "ATTRIBUTES"]
 
+from .merl import Merl  # noqa: E402  -- measured data: constructed from a file, not from attributes
+
+__all__.append("Merl")
+
 for _name in model_names():
-    if _name.isidentifier():          # Aggregate<Lambertian,X> entries are built with Aggregate(...)
+    if _name.isidentifier() and _name != "Merl":          # Aggregate<Lambertian,X> entries are built with Aggregate(...)
         globals()[_name] = _make_ctor(_name)
         __all__.append(_name)
 del _name

@@ -48,6 +48,7 @@ SIGNATURES = {
     "bbm_hip_loss_pairs": (_I, [_I, _P, _I, _I, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _U32, _U32, _P, _P, _SZ,
                                 _P]),
     "bbm_hip_epd_g1_table": (_I, [_P, _I]),
+    "bbm_hip_merl_table": (_I, [_P, _U32, _U32, _U32, _P, _P]),
     "bbm_hip_check_workspace_size": (_SZ, [_P]),
     "bbm_hip_check": (_I, [_I, _P, _I, _P, _P, _P, _P, _SZ, _P]),
     "bbm_hip_check_draws": (_I, [_I, _U64, _I, _I, _U64, _SZ, _P, _P, _P]),

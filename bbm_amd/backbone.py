@@ -364,6 +364,10 @@ def fromString(s):
     roughness = 0.1, eta = 1.3)' or 'Aggregate(Lambertian(...), Bagher(...))'
     (bsdf_string_convert.h:52-82 / bsdf_import.h:22-26).  Attributes may appear in any order;
     missing ones keep their defaults."""
+    mm = re.fullmatch(r'\s*Merl\(\s*"([^"]*)"\s*\)\s*', s)
+    if mm:          # merl_data's string form, Merl("filename") (merl.h:60, :161-164)
+        from .merl import Merl
+        return Merl(mm.group(1))
     tok = _tokenize(s)
     m, i = _parse_model(tok, 0, s)
     if i != len(tok):

@@ -30,6 +30,7 @@ BBM_HIP_SPECTRAL_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_AGGREGATE_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_EPD_MODELS(BBM_HIP_EXTERN)
 BBM_HIP_HE_MODELS(BBM_HIP_EXTERN)
+BBM_HIP_MERL_MODELS(BBM_HIP_EXTERN)
 int epd_table_host(float* out, int capacity);
 
 namespace {
@@ -140,6 +141,10 @@ const ModelEntry kSingle[] = {
   BBM_HIP_HE_ENTRY("HeHolzschuch", HeHolzschuchM),
   {"NganHe", 6, kFlagSpecular, &launch_eval_pdf<NganHeM>, &launch_sample<NganHeM>, &launch_reflectance<NganHeM>, &launch_loss<NganHeM>, &launch_check<NganHeM>,
    {0.5f, 0.5f, 0.5f, 0.18f, 3.0f, 1.3f}, {0, 0, 0, 0, 0, 1}, {1, 1, 1, kFMax, kFMax, 5}, "sssppp"},
+  // Merl (staticmodel/merl.h:224-225): no attributes in the reference (the data comes from a file); the two
+  // slots hold the device address of a table built by bbm_hip_merl_table, flagged Dependent so no fit moves them
+  {"Merl", 2, kFlagAll, &launch_eval_pdf<Merl>, &launch_sample<Merl>, &launch_reflectance<Merl>, &launch_loss<Merl>, &launch_check<Merl>,
+   {0, 0}, {0, 0}, {0, 0}, "xx"},
 };
 constexpr int kNumSingle = int(sizeof(kSingle) / sizeof(kSingle[0]));
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
@@ -670,6 +675,16 @@ int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprob
 int bbm_hip_epd_g1_table(float* out, int capacity)
 {
   return epd_table_host(out, capacity);
+}
+
+int bbm_hip_merl_table(const double* raw, uint32_t theta_h, uint32_t theta_d, uint32_t phi_d, float* table,
+                       void* stream)
+{
+  if (!raw || !table) return fail(BBM_HIP_ERR_INVALID_ARG, "bbm_hip_merl_table: null pointer");
+  if (theta_h != uint32_t(kMerlThetaH) || theta_d != uint32_t(kMerlThetaD) || phi_d != uint32_t(kMerlPhiD))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "BBM: not a recognized MERL BRDF (dimensions " + std::to_string(theta_h) + " x " +
+                                         std::to_string(theta_d) + " x " + std::to_string(phi_d) + ", expected 90 x 90 x 180)");
+  return merl_table_launch(raw, table, static_cast<hipStream_t>(stream));
 }
 
 size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* d)

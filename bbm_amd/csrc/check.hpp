@@ -268,6 +268,7 @@ template<class Model>
 int launch_check(int test, const CheckArgs& a0, double* acc, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  if (const int rc = host_validate<Model>::run(a0.p)) return rc;
   CheckArgs a = a0;
   void* scratch = nullptr;
   if (const int rc = host_params<Model>::run(a.p, kFlagAll, s, &scratch)) return rc;

@@ -53,6 +53,47 @@ __device__ __forceinline__ float std_lerpf(float a, float b, float t)
   return ((t > 1) == (b > a)) ? ((b < x) ? x : b) : ((x < b) ? x : b);
 }
 
+// ndf::sampler<NDF, 90, 1> (include/ndf/sampler.h), the data-driven importance sampler bbm::ndf_sampler
+// wraps around the He family and Merl (bbm/ndf_sampler.h:22-164), over a per-launch 90-bin CDF:
+// ndf::sampler::pdf (ndf/sampler.h:102-128) of the halfway vector m
+__device__ __forceinline__ float ndf_sampler_pdf(const float* __restrict__ cdf, v3 m)
+{
+  const float theta = theta_of(m);
+  const float ti = float(double(sqrtf(theta / kPiHalfF) * float(kHeBins)) - 0.5);
+  const float w = ti - floorf(ti);
+  const float fl = floorf(ti), ce = ceilf(ti);
+  // clamp(cast<Size_t>(floor(ti)), 0, 89): a negative float cast to size_t wraps on x86-64 (-> 89)
+  const int lidx = (fl < 0) ? kHeBins - 1 : min(int(fl), kHeBins - 1);
+  const int uidx = (ce < 0) ? kHeBins - 1 : min(int(ce), kHeBins - 1);
+  auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0f); };
+  const float p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
+  float st, ct;
+  cossin_cr(theta, ct, st);
+  const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * fabsf(st)) * kPi2F;
+  return ((m.z > 0) && (jac > kEpsF)) ? div_nr(p, jac) : 0.0f;
+}
+
+// ndf::sampler::sample (ndf/sampler.h:63-92): the sampled halfway vector for (xi0, xi1)
+__device__ __forceinline__ v3 ndf_sampler_halfway(const float* __restrict__ cdf, float xi0, float xi1)
+{
+  // cdf::sample (util/cdf.h:73-83): lower_bound of xi0, residual within the bin
+  int idx = 0;
+  while (idx < kHeBins && cdf[idx] < xi0) ++idx;
+  const bool valid = idx < kHeBins;
+  const float ev = valid ? cdf[idx] : 0.0f;
+  const float prev = (valid && idx >= 1) ? cdf[idx - 1] : 0.0f;
+  const float cp = ev - prev;
+  const float residual = valid ? (xi0 - prev) / cp : 0.0f;
+  const double xr = fabs(double(residual) - 0.5);
+  const double off = 1 - safe_sqrt(1 - 2 * xr);
+  const double sgn = copysign(1.0, double(residual) - 0.5);
+  const double q = (double(idx) + 0.5 + sgn * off) / double(kHeBins);
+  float theta = float(q * q * double(kPiHalfF));
+  const float phi = kPi2F * xi1;
+  theta = (theta > kPiHalfF) ? kPiF - theta : theta;
+  return sph_to_vec(phi, theta);
+}
+
 // fresnel::complex<CONF, Spectrum> per channel (include/bbm/fresnel_complex.h:38-63); params = n RGB, k RGB
 struct FresnelComplexRGB
 {
@@ -282,22 +323,7 @@ struct He
   }
 
   // ndf::sampler::pdf (ndf/sampler.h:102-128) of the halfway vector m
-  __device__ __forceinline__ float sampler_pdf(v3 m) const
-  {
-    const float theta = theta_of(m);
-    const float ti = float(double(sqrtf(theta / kPiHalfF) * float(kHeBins)) - 0.5);
-    const float w = ti - floorf(ti);
-    const float fl = floorf(ti), ce = ceilf(ti);
-    // clamp(cast<Size_t>(floor(ti)), 0, 89): a negative float cast to size_t wraps on x86-64 (-> 89)
-    const int lidx = (fl < 0) ? kHeBins - 1 : min(int(fl), kHeBins - 1);
-    const int uidx = (ce < 0) ? kHeBins - 1 : min(int(ce), kHeBins - 1);
-    auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0f); };
-    const float p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
-    float st, ct;
-    cossin_cr(theta, ct, st);
-    const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * fabsf(st)) * kPi2F;
-    return ((m.z > 0) && (jac > kEpsF)) ? div_nr(p, jac) : 0.0f;
-  }
+  __device__ __forceinline__ float sampler_pdf(v3 m) const { return ndf_sampler_pdf(cdf, m); }
 
   template<int MODE>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
@@ -336,22 +362,7 @@ struct He
   {
     dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
     if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1) && (out.z > 0)) || masked(component)) return;
-    // cdf::sample (util/cdf.h:73-83): lower_bound of xi0, residual within the bin
-    int idx = 0;
-    while (idx < kHeBins && cdf[idx] < xi0) ++idx;
-    const bool valid = idx < kHeBins;
-    const float ev = valid ? cdf[idx] : 0.0f;
-    const float prev = (valid && idx >= 1) ? cdf[idx - 1] : 0.0f;
-    const float cp = ev - prev;
-    const float residual = valid ? (xi0 - prev) / cp : 0.0f;
-    const double xr = fabs(double(residual) - 0.5);
-    const double off = 1 - safe_sqrt(1 - 2 * xr);
-    const double sgn = copysign(1.0, double(residual) - 0.5);
-    const double q = (double(idx) + 0.5 + sgn * off) / double(kHeBins);
-    float theta = float(q * q * double(kPiHalfF));
-    const float phi = kPi2F * xi1;
-    theta = (theta > kPiHalfF) ? kPiF - theta : theta;
-    const v3 h = sph_to_vec(phi, theta);
+    const v3 h = ndf_sampler_halfway(cdf, xi0, xi1);
     // reflect(out, h) = h dot(h, out) 2.0 - out (core/vec_transform.h:43-44)
     const float d = dot3(h, out);
     dir = mk3(2.0f * (h.x * d) - out.x, 2.0f * (h.y * d) - out.y, 2.0f * (h.z * d) - out.z);
@@ -394,22 +405,30 @@ __global__ __launch_bounds__(128) void k_he_cdf(ParamBlock p, uint32_t component
   }
 }
 
+// Builds the launch's CDF into stream-ordered scratch and stores its address (two slots) and the component
+// it was built for after the model's kParams parameters (M::kParams + 0..2).
+template<class M>
+int ndf_sampler_cdf_run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch, const char* who)
+{
+  float* cdf = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&cdf), kHeBins * sizeof(float), s);
+  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: hipMallocAsync: " + hipGetErrorString(e));
+  hipLaunchKernelGGL((k_he_cdf<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
+  if ((e = hipGetLastError()) != hipSuccess)
+    return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: launch: " + hipGetErrorString(e));
+  set_param_ptr(p.v, M::kParams, cdf);
+  __builtin_memcpy(p.v + M::kParams + 2, &component, 4);
+  *scratch = cdf;
+  return BBM_HIP_OK;
+}
+
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
 {
   using M = He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>;
   static int run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch)
   {
-    float* cdf = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&cdf), kHeBins * sizeof(float), s);
-    if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("He sampler CDF: hipMallocAsync: ") + hipGetErrorString(e));
-    hipLaunchKernelGGL((k_he_cdf<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
-    if ((e = hipGetLastError()) != hipSuccess)
-      return fail(BBM_HIP_ERR_HIP, std::string("He sampler CDF: launch: ") + hipGetErrorString(e));
-    set_param_ptr(p.v, M::kParams, cdf);
-    __builtin_memcpy(p.v + M::kParams + 2, &component, 4);
-    *scratch = cdf;
-    return BBM_HIP_OK;
+    return ndf_sampler_cdf_run<M>(p, component, s, scratch, "He");
   }
   static void done(void* scratch, hipStream_t s) { if (scratch) (void)hipFreeAsync(scratch, s); }
 };

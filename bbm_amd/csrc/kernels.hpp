@@ -35,6 +35,10 @@ struct ParamBlock { float v[kMaxParams]; };
 // Per-model host work before a launch (e.g. building a lookup table on first use); no-op by default.
 template<class Model> struct host_prepare { static int run(hipStream_t) { return 0; } };
 
+// Per-launch check of a parameter block before anything is enqueued (e.g. a table address that must be set);
+// no-op by default.
+template<class Model> struct host_validate { static int run(const ParamBlock&) { return 0; } };
+
 // Per-launch derived data a model's sample / pdf need (e.g. a data-driven sampling CDF), enqueued on the
 // launch stream and passed in the parameter block after the model's own parameters; `done` releases the
 // stream-ordered scratch after the launch.  No-op by default.
@@ -382,6 +386,7 @@ template<class Model, int MODE, bool MASK>
 int launch_mode(const EvalArgs& a0, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  if (const int rc = host_validate<Model>::run(a0.p)) return rc;
   EvalArgs a = a0;
   void* scratch = nullptr;
   if (MODE & kModePdf)
@@ -419,6 +424,7 @@ template<class Model, bool MASK>
 int launch_sample_mask(const SampleArgs& a0, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  if (const int rc = host_validate<Model>::run(a0.p)) return rc;
   SampleArgs a = a0;
   void* scratch = nullptr;
   if (const int rc = host_params<Model>::run(a.p, a.component, s, &scratch)) return rc;
@@ -486,6 +492,7 @@ template<class Model>
 int launch_reflectance(const ReflArgs& a, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
+  if (const int rc = host_validate<Model>::run(a.p)) return rc;
   uint64_t blocks = (a.n + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();

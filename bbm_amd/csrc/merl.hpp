@@ -1,0 +1,145 @@
+// bbm_amd/csrc/merl.hpp -- the MERL-MIT measured BRDF (include/staticmodel/merl.h) on the GPU:
+//   Merl = ndf_sampler< merl_data<CONF, "Merl">, 90, 1 >                      (merl.h:224-225)
+// eval is a table lookup: merl_linearizer's forward map (in, out) -> (theta_h, theta_d, phi_d) bin
+// (linearizer/merl_linearizer.h:93-125) into the 90 x 90 x 180 table the reference reads from a MERL
+// .binary file and white-balances (merl.h:173-206).  The table lives in HBM as float4 (r, g, b, 0) --
+// the reference's color<double> entries rounded to float exactly as lookup<Spectrum> does (merl.h:95) --
+// so one pair costs one 16 B gather; it is built on the GPU from the file's doubles by bbm_hip_merl_table
+// and its device address travels in parameter slots 0-1.  sample / pdf are the data-driven ndf_sampler
+// over the backscatter eval(h, h) (bbm/ndf_sampler.h:22-164), shared with the He family (he.hpp);
+// reflectance is merl_data's placeholder, 1 for component All (merl.h:149-156).
+#pragma once
+#include "he.hpp"    // ndf_sampler_pdf / ndf_sampler_halfway / ndf_sampler_cdf_run, param_ptr
+
+namespace bbmhip {
+
+constexpr int kMerlThetaH = 90, kMerlThetaD = 90, kMerlPhiD = 180;   // merl.h:184, merl_linearizer.h:28
+constexpr uint32_t kMerlSize = uint32_t(kMerlThetaH) * kMerlThetaD * kMerlPhiD;
+
+// merl_linearizer::operator()(in, out, mask) (linearizer/merl_linearizer.h:93-125) for samplesH = (1, 90),
+// samplesD = (180, 90); the caller has checked z(in) >= 0 && z(out) >= 0.
+__device__ __forceinline__ uint32_t merl_index(v3 in, v3 out)
+{
+  // convertToHalfwayDifference (core/vec_transform.h:90-97): half = normalize(in + out),
+  // diff = rotationY(-theta_h) * (rotationZ(-phi_h) * in); matrix rows from transform.h:47-81
+  const v3 half = halfway(in, out);
+  const float h_phi = phi_of(half), h_th = theta_of(half);
+  float cz, sz, cy, sy;
+  cossin_cr(-h_phi, cz, sz);
+  cossin_cr(-h_th, cy, sy);
+  const v3 t = mk3(((0.0f + cz * in.x) + -sz * in.y) + 0.0f * in.z,
+                   ((0.0f + sz * in.x) + cz * in.y) + 0.0f * in.z,
+                   ((0.0f + 0.0f * in.x) + 0.0f * in.y) + 1.0f * in.z);
+  const v3 d = mk3(((0.0f + cy * t.x) + 0.0f * t.y) + sy * t.z,
+                   ((0.0f + 0.0f * t.x) + 1.0f * t.y) + 0.0f * t.z,
+                   ((0.0f + -sy * t.x) + 0.0f * t.y) + cy * t.z);
+  float d_phi = phi_of(d);
+  const float d_th = theta_of(d);
+  // phi_d is unstable for in ~= out; reciprocity folds it into [0, pi)
+  if (dot3(in, out) > 1.0f - kEpsF) d_phi = 0.0f;
+  if (d_phi >= kPiF) d_phi = d_phi - kPiF;
+  // idx = floor((coord / Sphere(0.5) + eps) * samples), theta_h through a sqrt; clamp to the table
+  const float ip = floorf((__fdiv_rn(d_phi, kPiF) + kEpsF) * float(kMerlPhiD));
+  const float it = floorf((__fdiv_rn(d_th, kPiHalfF) + kEpsF) * float(kMerlThetaD));
+  const float ih = floorf(safe_sqrtf(__fdiv_rn(h_th, kPiHalfF) + kEpsF) * float(kMerlThetaH));
+  const int ipc = int(clampf(ip, 0.0f, float(kMerlPhiD - 1)));
+  const int itc = int(clampf(it, 0.0f, float(kMerlThetaD - 1)));
+  const int ihc = int(clampf(ih, 0.0f, float(kMerlThetaH - 1)));
+  return uint32_t((ihc * kMerlThetaD + itc) * kMerlPhiD + ipc);
+}
+
+struct Merl
+{
+  static constexpr int kParams = 2;                      // device address of the float4 table
+  static constexpr uint32_t kComponent = kFlagAll;
+  const float4* table;
+  const float* cdf;             // kHeBins floats for the launch's component (ndf_sampler_cdf_run)
+  uint32_t launch_component;
+
+  __device__ explicit Merl(const float* p)
+  {
+    table = reinterpret_cast<const float4*>(param_ptr(p, 0));
+    cdf = param_ptr(p, kParams);
+    __builtin_memcpy(&launch_component, p + kParams + 2, 4);
+  }
+
+  __device__ __forceinline__ bool masked(uint32_t component) const { return component != launch_component; }
+
+  // merl_data::eval (merl.h:78-96): mask is_set(component, All) -- every bit of All set (util/flags.h:100-103),
+  // so only component All -- and z(in) >= 0 && z(out) >= 0 (not strict)
+  template<bool SCALE = true>
+  __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
+  {
+    rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    // the table check is wave-uniform; it only matters for probe vectors the host cannot see (fit loss)
+    if (((component & kFlagAll) == kFlagAll) && (in.z >= 0) && (out.z >= 0) && table)
+    {
+      const float4 v = table[merl_index(in, out)];
+      rgb[0] = v.x; rgb[1] = v.y; rgb[2] = v.z;
+    }
+  }
+
+  template<int MODE>
+  __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
+  {
+    if (MODE & kModeEval) eval_rgb(in, out, component, rgb);
+    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    if (MODE & kModePdf)
+    {
+      // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156)
+      const bool active = (out.z > 0) && (in.z > 0) && !masked(component);
+      const v3 h = halfway(in, out);
+      const float p = float(double(ndf_sampler_pdf(cdf, h)) / fabs(4.0 * double(dot3(out, h))));
+      pdf = active ? p : 0.0f;
+    }
+    else pdf = 0.0f;
+  }
+
+  // merl_data::reflectance (merl.h:149-156): a placeholder, 1 where is_set(component, All)
+  __device__ __forceinline__ void reflectance(v3, uint32_t component, float* rgb) const
+  {
+    const float v = ((component & kFlagAll) == kFlagAll) ? 1.0f : 0.0f;
+    rgb[0] = rgb[1] = rgb[2] = v;
+  }
+
+  // ndf_sampler::sample (bbm/ndf_sampler.h:78-111)
+  __device__ __forceinline__ void sample(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1) && (out.z > 0)) || masked(component)) return;
+    const v3 h = ndf_sampler_halfway(cdf, xi0, xi1);
+    const float d = dot3(h, out);
+    dir = mk3(2.0f * (h.x * d) - out.x, 2.0f * (h.y * d) - out.y, 2.0f * (h.z * d) - out.z);
+    float rgb[3];
+    eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
+    flag = component;
+  }
+};
+
+template<>
+struct host_validate<Merl>
+{
+  static int run(const ParamBlock& p)
+  {
+    if (!param_ptr(p.v, 0))
+      return fail(BBM_HIP_ERR_INVALID_ARG, "Merl: parameters hold no table (build one with bbm_hip_merl_table)");
+    return BBM_HIP_OK;
+  }
+};
+
+template<>
+struct host_params<Merl>
+{
+  static int run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch)
+  {
+    return ndf_sampler_cdf_run<Merl>(p, component, s, scratch, "Merl");
+  }
+  static void done(void* scratch, hipStream_t s) { if (scratch) (void)hipFreeAsync(scratch, s); }
+};
+
+// merl_data::import (merl.h:173-206): channel c of entry i is max(0, raw[c * size + i] * w_c / 1500.0) in
+// double, w = (1.0, 1.15, 1.66), rounded to float by lookup<Spectrum>.
+int merl_table_launch(const double* raw, float* table, hipStream_t s);
+
+}  // namespace bbmhip

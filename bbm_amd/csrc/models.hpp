@@ -9,6 +9,7 @@
 #include "aggregate.hpp"
 #include "epd.hpp"
 #include "he.hpp"
+#include "merl.hpp"
 
 namespace bbmhip {
 
@@ -64,6 +65,7 @@ using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 #define BBM_HIP_SPECTRAL_MODELS(X) X(Bagher)
 #define BBM_HIP_EPD_MODELS(X) X(EpdM)
 #define BBM_HIP_HE_MODELS(X) X(HeM) X(HeWestinM) X(HeHolzschuchM) X(NganHeM)
+#define BBM_HIP_MERL_MODELS(X) X(Merl)
 #define BBM_HIP_AGGREGATE_MODELS(X) \
   X(AggBagherM) X(AggCookTorranceM) X(AggGGXM) X(AggLowASM) X(AggLowMicrofacetM) X(AggLowSmoothM) X(AggNganASM) \
   X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM)

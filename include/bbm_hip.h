@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 4
+#define BBM_HIP_ABI_VERSION 5
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -186,6 +186,16 @@ int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprob
  * restating its generator (precompute/HolzschuchPacanowski/G1.cpp).  Copies min(capacity, 100000)
  * entries to host memory `out` (may be NULL) and returns the table size, or a negative error code. */
 int bbm_hip_epd_g1_table(float* out, int capacity);
+
+/* Merl (include/staticmodel/merl.h): build the model's device table from a MERL-MIT .binary file.
+ * Replaces merl_data::import (merl.h:173-206).  `raw` = device copy of the 3 x theta_h x theta_d x phi_d
+ * doubles that follow the file's three uint32 dimensions (channel planes R, G, B); `table` = device
+ * buffer of theta_h*theta_d*phi_d float4 (16 B) entries, filled with (max(0, R/1500), max(0, 1.15 G/1500),
+ * max(0, 1.66 B/1500), 0) rounded to float.  Dimensions other than 90 x 90 x 180 are rejected as in the
+ * reference.  The Merl model's two parameters are the table's device address (low, high 32 bits). */
+#define BBM_HIP_MERL_ENTRIES (90u * 90u * 180u)
+int bbm_hip_merl_table(const double* raw, uint32_t theta_h, uint32_t theta_d, uint32_t phi_d, float* table,
+                       void* stream);
 
 /* ---------------------------------------------------------------- synthetic directions */
 

@@ -4,3 +4,4 @@
 #include "ref_harness.cpp"
 #include "ref_fit.cpp"
 #include "ref_check.cpp"
+#include "ref_merl.cpp"

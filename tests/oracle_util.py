@@ -307,3 +307,68 @@ def merl_directions_f64(h=(1, 90), d=(180, 90)):
     din[2] = np.maximum(din[2], 0)
     dout[2] = np.maximum(dout[2], 0)
     return din, dout
+
+
+# ------------------------------------------------------------------------------------------ Merl
+
+def synthetic_merl(path, seed=20240611):
+    """Write a synthetic MERL-MIT .binary (no measured data ships with the reference): a smooth
+    specular-plus-diffuse table over (theta_h, theta_d, phi_d) with noise, and 2 % of the entries set to
+    -1 as in the measured files' unmeasured bins (merl.h:200-202 clamps them to 0).  Returns the raw
+    (3, 90, 90, 180) float64 array."""
+    from bbm_amd.merl import write_binary
+    rng = np.random.default_rng(seed)
+    th, td, pd = np.meshgrid(np.arange(90) / 90.0, np.arange(90) / 90.0, np.arange(180) / 180.0, indexing="ij")
+    rgb = np.empty((3, 90, 90, 180))
+    for c, (a, b) in enumerate(((900.0, 60.0), (700.0, 90.0), (400.0, 120.0))):
+        rgb[c] = a * np.exp(-8.0 * th * th) * (1 + 0.5 * np.cos(2 * np.pi * pd)) + b * (1 + td) \
+            + rng.normal(0.0, 5.0, th.shape)
+    rgb[rng.random(rgb.shape) < 0.02] = -1.0
+    write_binary(path, rgb)
+    return rgb
+
+
+def merl_table_numpy(raw):
+    """merl_data::import's white balance (merl.h:199-203) in float64, rounded to float as lookup<Spectrum>
+    does: (3, 90*90*180) float32."""
+    raw = raw.reshape(3, -1)
+    w = (1.0, 1.15, 1.66)
+    return np.stack([np.fmax(0.0, raw[c] * w[c] / 1500.0) for c in range(3)]).astype(np.float32)
+
+
+def ref_merl_eval_pdf(filename, din, dout, component=3, unit=0, nthreads=8):
+    lib = ref()
+    din = np.ascontiguousarray(din, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n = din.shape[1]
+    res = np.zeros((4, n), np.float32)
+    rc = lib.bbmref_merl_eval_pdf(str(filename).encode(), ctypes.c_size_t(n), _fp(din[0]), _fp(din[1]), _fp(din[2]),
+                                  _fp(dout[0]), _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component),
+                                  ctypes.c_uint32(unit), 3, _fp(res[0]), _fp(res[1]), _fp(res[2]), _fp(res[3]),
+                                  nthreads)
+    if rc != 0:
+        raise RuntimeError(f"reference rejected MERL file {filename}")
+    return res
+
+
+def ref_merl_sample(filename, dout, xi, component=3, unit=0):
+    lib = ref()
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    xi = np.ascontiguousarray(xi, dtype=np.float32)
+    n = dout.shape[1]
+    d = np.zeros((4, n), np.float32)
+    flag = np.zeros(n, np.uint32)
+    rc = lib.bbmref_merl_sample(str(filename).encode(), ctypes.c_size_t(n), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]),
+                                _fp(xi[0]), _fp(xi[1]), ctypes.c_uint32(component), ctypes.c_uint32(unit),
+                                _fp(d[0]), _fp(d[1]), _fp(d[2]), _fp(d[3]), _fp(flag))
+    if rc != 0:
+        raise RuntimeError(f"reference rejected MERL file {filename}")
+    return d, flag
+
+
+def ref_merl_to_string(filename):
+    lib = ref()
+    buf = ctypes.create_string_buffer(4096)
+    if lib.bbmref_merl_to_string(str(filename).encode(), buf, 4096) < 0:
+        raise RuntimeError(f"reference rejected MERL file {filename}")
+    return buf.value.decode()

@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 4
+    assert lib.bbm_hip_abi_version() == 5
 
 
 def test_registry_matches_reference(lib):
@@ -52,6 +52,8 @@ def test_registry_matches_reference(lib):
     names = [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
     assert "CookTorrance" in names and "GGX" in names and "Lambertian" in names
     for i, name in enumerate(names):
+        if name == "Merl":        # measured data, no attributes in the reference: tests/test_merl.py
+            continue
         ref = META["models"][name]
         assert lib.bbm_hip_model_id(name.encode()) == i
         k = lib.bbm_hip_model_nparams(i)
@@ -72,8 +74,10 @@ def test_python_mirror_layout_covers_every_reference_model():
 def test_param_attrs_match_reference(lib):
     """bsdf_attr flags per parameter == what bbm::parameter_values(model, flag) selects in the reference."""
     names = [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
-    assert set(names) == set(META["models"])
+    assert set(names) - {"Merl"} == set(META["models"])
     for i, name in enumerate(names):
+        if name == "Merl":        # measured data, no attributes in the reference: tests/test_merl.py
+            continue
         ref = META["models"][name]["attrs"]
         buf = (ctypes.c_uint32 * 64)()
         assert lib.bbm_hip_model_param_attrs(i, buf, 64) == len(ref)
@@ -123,7 +127,7 @@ def test_to_string_matches_bbm_toString(name):
 def test_from_string_round_trip_and_named_args():
     import bbm_amd
     for name in bbm_amd.model_names():
-        for s in META["models"][name]["strings"]:
+        for s in META["models"].get(name, {"strings": []})["strings"]:
             m = bbm_amd.fromString(s)
             assert str(m) == s
     m = bbm_amd.fromString("CookTorrance(eta = 1.5, roughness = 0.2)")
