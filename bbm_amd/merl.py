@@ -47,6 +47,17 @@ def write_binary(filename, rgb):
         rgb.tofile(f)
 
 
+WHITE_BALANCE = (1.0, 1.15, 1.66)   # merl.h:200-202: channel c of the table is max(0, raw_c * w_c / 1500)
+
+
+def encode(rgb):
+    """Inverse of the import's white balance: a (3, 90*90*180) table of BRDF values (e.g. an analytic
+    model evaluated at the merl_linearizer bin centres) -> the (3, 90, 90, 180) raw doubles a MERL
+    .binary holds."""
+    rgb = np.asarray(rgb, dtype=np.float64).reshape(3, -1)
+    return np.stack([rgb[c] * 1500.0 / WHITE_BALANCE[c] for c in range(3)]).reshape((3,) + DIMS)
+
+
 class Merl(BsdfModel):
     """Merl(filename) -- bbm::merl<floatRGB> (staticmodel/merl.h:224-225) on the current CUDA device."""
 

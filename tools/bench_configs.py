@@ -2,26 +2,30 @@
 
   models  (config 3) every single bsdfmodel's eval over 10M shared pairs per GPU, one launch per model
           (bbm_hip_eval).  Algorithmic bytes: 24 B in + 12 B RGB out = 36 B/pair (models that read only
-          z: 8 + 12 = 20 B).  Per-model pairs/s and fraction of the 8 TB/s HBM roofline.
+          z: 8 + 12 = 20 B).  Per-model pairs/s and fraction of the 8 TB/s HBM roofline.  Merl (measured data,
+          a synthetic MERL .binary) also gathers one 16 B table entry per pair from its 23 MB table, which
+          the L2/MALL serve; the 36 B/pair figure leaves that gather out.
   sample  (config 4) importance-sample -> eval -> pdf Monte-Carlo loop (checkBsdf's reflectance test,
           bbm_hip_check REFLECTANCE with importance sampling) for the microfacet models CookTorrance and
           GGX: 125M samples per GPU (1B over 8 GPUs), 8 theta_out slots, reduced in-kernel to per-slot
           sums -- no HBM traffic per sample, so the kernel is VALU-bound: reported as samples/s.
-  fit     (config 5) the fitting loss of one compass step: Aggregate(Lambertian, Bagher) against a
-          reference table on the MERL grid (90 x 90 x 180 = 1.458M pairs, sharded over the GPUs),
+  fit     (config 5) the fitting loss of one compass step: Aggregate(Lambertian, Bagher) against a Merl
+          reference (a MERL .binary holding a perturbed Bagher fit, read through bbm_amd.Merl) on the MERL grid (90 x 90 x 180 = 1.458M pairs, sharded over the GPUs),
           2P = 36 probes in one bbm_hip_loss launch, plus the RCCL all-reduce of the 36 partial sums
           when N > 1 (strong scaling: the grid is fixed).  Reported as probe-pair evaluations/s.
 Timing follows bench.py: warmup, barrier + synchronize around K timed steps, max over ranks.
 """
 import ctypes
 import json
+import os
+import tempfile
 import time
 
 import numpy as np
 import torch
 
 import bbm_amd
-from bbm_amd import _lib, check, fit
+from bbm_amd import _lib, check, fit, merl
 from bbm_amd.backbone import _stream_ptr
 
 SEED = 0xBB5EED
@@ -76,7 +80,7 @@ def bench_models(args, dist, rank, world):
     total_t = 0.0
     names = [m for m in bbm_amd.model_names() if not m.startswith("Aggregate")]
     for name in names:
-        m = bbm_amd.BsdfModel(name)
+        m = _merl_from(bbm_amd.CookTorrance()) if name == "Merl" else bbm_amd.BsdfModel(name)
         elapsed, kern_ms = _timed(lambda: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=stream), args, dist, stream)
         bpp = 20 if name in Z_ONLY else 36
         gbs = bpp * n / (kern_ms * 1e-3) / 1e9
@@ -131,13 +135,24 @@ def bench_sample(args, dist, rank, world):
               {"scaling": "weak", "per_model": res, "roofline": {"bound": "valu", "note": "no per-sample HBM traffic"}})
 
 
+def _merl_from(source):
+    """A Merl model read from a MERL-format .binary that holds `source` evaluated at the MERL bin centres."""
+    din, dout = fit.merl_linearizer().directions()
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "synthetic.binary")
+        merl.write_binary(path, merl.encode(source.eval(din, dout).cpu().numpy()))
+        return bbm_amd.Merl(path)
+
+
 def bench_fit(args, dist, rank, world):
     name = "Aggregate<Lambertian,Bagher>"
     fitted = bbm_amd.BsdfModel(name)
-    reference = bbm_amd.BsdfModel(name)
-    p = reference.parameter_values()
-    reference.set_parameter_values((p * np.float32(1.1)).astype(np.float32))
     lin = fit.merl_linearizer()
+    # the measured reference: a MERL-format .binary (no measured data ships with the reference repo) holding a
+    # perturbed Bagher fit at the MERL bin centres, read back through bbm_amd.Merl like a real MERL file
+    source = bbm_amd.BsdfModel(name)
+    source.set_parameter_values((source.parameter_values() * np.float32(1.1)).astype(np.float32))
+    reference = _merl_from(source)
     loss = fit.SampledLoss(fitted, reference, "standardLog", lin, dist=dist)
     idx = fitted.parameter_indices(fit.ALL)
     probes = np.repeat(fitted.parameter_values()[None], 2 * len(idx), axis=0)
@@ -150,7 +165,8 @@ def bench_fit(args, dist, rank, world):
         pairs = lin.size()
         _line(args, world, "fitting-loss probe-pair evals/s, Aggregate(Lambertian, Bagher), MERL grid, 2P probes per "
               "compass step (config 5)", len(probes) * pairs * args.steps / elapsed, "probe-pairs/s", elapsed,
-              {"workload": f"{len(probes)} probes x {pairs} MERL pairs per compass step (standardLog), sharded grid",
+              {"workload": f"{len(probes)} probes x {pairs} MERL pairs per compass step (standardLog), sharded grid; "
+                           "reference = Merl model read from a synthetic MERL .binary",
                "probes": len(probes), "pairs": pairs, "parallelism": f"dp{world} (grid shards, all-reduce of "
                                                                       f"{len(probes)} doubles per step)"},
               {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms})
