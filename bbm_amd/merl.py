@@ -73,7 +73,7 @@ class Merl(BsdfModel):
         self.table = torch.empty((int(np.prod(dims)), 4), dtype=torch.float32, device=dev)
         _lib.check(lib.bbm_hip_merl_table(ctypes.c_void_p(raw_dev.data_ptr()), dims[0], dims[1], dims[2],
                                           ctypes.c_void_p(self.table.data_ptr()), _stream_ptr(stream)))
-        torch.cuda.current_stream().synchronize() if stream is None else stream.synchronize()
+        (torch.cuda.current_stream() if stream is None else stream).synchronize()   # raw_dev is freed next
         del raw_dev
         self.name = "Merl"
         self.model_id = mid

@@ -15,4 +15,7 @@ for W in models sample fit; do
   timeout -k 10 300 python bench.py --workload $W --steps 10 --warmup 3 > gpurun_out/final/bench_$W.json 2> gpurun_out/final/bench_$W.err || { echo "bench $W failed"; tail -20 gpurun_out/final/bench_$W.err; exit 1; }
   cut -c1-200 gpurun_out/final/bench_$W.json
 done
-find gpurun_out/final/prof -name "*kernel_stats.csv" | head -3
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof_models" -o run -- python3 "$R/bench.py" --workload models --steps 5 --warmup 2 > "$R/gpurun_out/final/prof_models.log" 2>&1 || { echo "rocprof models failed"; tail -20 "$R/gpurun_out/final/prof_models.log"; exit 1; }
+cd "$R"
+find gpurun_out/final/prof gpurun_out/final/prof_models -name "*kernel_stats.csv" | head -3
