@@ -68,7 +68,7 @@ __device__ __forceinline__ float div_nr(float n, float d)
 }
 
 // exp(x) for a float x <= 0 to ~1 ulp without the library's range checks: x log2(e) split in a head (rounded
-// product) and tail (its fma residual + x times log2(e)'s own tail), v_exp_f32 of the head, first-order fix-up
+// product) and tail (its fma residual + x times log2(e)'s own tail, one fused op), v_exp_f32 of the head, first-order fix-up
 // by the tail.  Results below the normal range flush to zero.
 __device__ __forceinline__ float expf_neg(float x)
 {
@@ -76,7 +76,7 @@ __device__ __forceinline__ float expf_neg(float x)
   constexpr float kLog2eLo = 1.925963033500011079e-08f;          // log2 e - kLog2eHi
   constexpr float kLn2 = 0.693147180559945309f;
   const float t = x * kLog2eHi;
-  const float e = __builtin_fmaf(x, kLog2eHi, -t) + x * kLog2eLo;
+  const float e = __builtin_fmaf(x, kLog2eLo, __builtin_fmaf(x, kLog2eHi, -t));
   const float r = __builtin_amdgcn_exp2f(t);
   return __builtin_fmaf(r, e * kLn2, r);
 }
