@@ -83,10 +83,39 @@ def _mask_ptr(mask, n):
     return mask.data_ptr(), mask
 
 
+def _out_rows(t, rows, n, device, what):
+    """Validate a caller-supplied output buffer before its row pointers reach a kernel: float32, on the
+    inputs' device, shape (rows, n) (or (n,) for rows == 0) with every row contiguous."""
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected a float32 CUDA tensor")
+    if not t.is_cuda or t.device != device:
+        raise ValueError(f"{what}: must live on {device}, got {t.device}")
+    shape = (n,) if rows == 0 else (rows, n)
+    if tuple(t.shape) != shape:
+        raise ValueError(f"{what}: expected shape {shape}, got {tuple(t.shape)}")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{what}: rows must be contiguous")
+    return t
+
+
 def _stream_ptr(stream):
     torch = _torch()
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
+
+
+def _on_stream(stream, *tensors):
+    """Tensors allocated here (outputs, the mask copy) but used by a launch on a stream other than the current
+    one: tell the caching allocator, so their memory is not reused before that stream has run the kernel."""
+    if stream is None:
+        return
+    torch = _torch()
+    if stream == torch.cuda.current_stream():
+        return
+    for t in tensors:
+        if t is not None:
+            t.record_stream(stream)
 
 
 def model_names():
@@ -228,12 +257,15 @@ class BsdfModel:
         ox, oy, oz, _ = _soa(out, n, what="out")
         mptr, _keep = _mask_ptr(mask, n)
         dev = torch.device("cuda", torch.cuda.current_device())
-        if mode & 1 and rgb is None:
-            rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
-        if mode & 2 and pdf is None:
-            pdf = torch.empty((n,), dtype=torch.float32, device=dev)
+        if mode & 1:
+            rgb = torch.empty((3, n), dtype=torch.float32, device=dev) if rgb is None else \
+                _out_rows(rgb, 3, n, dev, "rgb")
+        if mode & 2:
+            pdf = torch.empty((n,), dtype=torch.float32, device=dev) if pdf is None else \
+                _out_rows(pdf, 0, n, dev, "pdf")
         lib = _lib.load()
         s = _stream_ptr(stream)
+        _on_stream(stream, _keep, rgb, pdf)
         if mode == 3:
             rc = lib.bbm_hip_eval_pdf(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
                                       int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),
@@ -273,6 +305,7 @@ class BsdfModel:
         d = torch.empty((3, n), dtype=torch.float32, device=dev)
         p = torch.empty((n,), dtype=torch.float32, device=dev)
         f = torch.empty((n,), dtype=torch.int32, device=dev)
+        _on_stream(stream, _keep, d, p, f)
         lib = _lib.load()
         _lib.check(lib.bbm_hip_sample(self.model_id, self._pptr(), self._params.size, ox, oy, oz,
                                       x0.data_ptr(), x1.data_ptr(), mptr, n, int(component), int(unit),
@@ -285,7 +318,9 @@ class BsdfModel:
         torch = _torch()
         ox, oy, oz, n = _soa(out, what="out")
         mptr, _keep = _mask_ptr(mask, n)
-        rgb = torch.empty((3, n), dtype=torch.float32, device=out.device)
+        dev = (out[0] if isinstance(out, (tuple, list)) else out).device
+        rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
+        _on_stream(stream, _keep, rgb)
         lib = _lib.load()
         _lib.check(lib.bbm_hip_reflectance(self.model_id, self._pptr(), self._params.size, ox, oy, oz, mptr, n,
                                            int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),

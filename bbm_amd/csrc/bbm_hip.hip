@@ -600,7 +600,8 @@ int bbm_hip_linearize(const bbm_hip_linearizer* lin, uint64_t begin, size_t n,
 
 size_t bbm_hip_loss_workspace_size(int nprobes)
 {
-  return nprobes > 0 ? size_t(kLossMaxBlocks) * size_t(nprobes) * sizeof(double) : 0;
+  // per-block partial sums, then the probes' constructed models (kLossModelBytes each, 256-byte aligned)
+  return nprobes > 0 ? size_t(kLossMaxBlocks) * size_t(nprobes) * sizeof(double) + size_t(nprobes) * kLossModelBytes : 0;
 }
 
 namespace {
@@ -625,6 +626,7 @@ int loss_common(int model_id, const float* probes, int nparams, int nprobes, con
   a.probes = probes; a.nprobes = nprobes; a.stride = nparams; a.loss_kind = loss_kind;
   a.component = component & kFlagAll;
   a.block_sums = static_cast<double*>(workspace);
+  a.models = static_cast<char*>(workspace) + size_t(kLossMaxBlocks) * size_t(nprobes) * sizeof(double);
   a.sums = sums;
   return BBM_HIP_OK;
 }

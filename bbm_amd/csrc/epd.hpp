@@ -162,7 +162,7 @@ struct EpdNdf
   {
     const float c2 = h.z * h.z;
     const float t2 = div_nr(1 - c2, c2);
-    const float D = div_nr(normalization * expf(-powf(div_nr(t2, beta * beta), p)), c2 * c2);
+    const float D = div_nr(normalization * expf_dn(-powf_acc(div_nr(t2, beta * beta), p)), c2 * c2);
     return (h.z > 0) ? D : 0.0f;
   }
 
@@ -188,7 +188,7 @@ struct EpdNdf
     float sp, cp;
     cossin_cr(kPi2F * xi0, cp, sp);
     const float g = float(gamma_q_inv_d(double(inv_p), double(xi1)));
-    const float tan2 = beta * beta * powf(g, inv_p);
+    const float tan2 = beta * beta * powf_acc(g, inv_p);
     const float cosT = float(1.0 / sqrt(1.0 + double(tan2)));          // rsqrt(1.0 + tan2) in double, stored as Value
     const float sinT = float(safe_sqrt(1.0 - double(cosT * cosT)));
     return mk3(cp * sinT, sp * sinT, cosT);

@@ -215,6 +215,30 @@ struct He
     return (sigma0 > kEpsF) ? r : 0.0f;
   }
 
+  // The reference's Taylor terms m - 1 and m (he.h:452-455) rounded as it rounds them: gm chain in float with
+  // double factors g / m, eb / m in float, term in double with a double exp.  Term 0 is the loop's initial 0.
+  struct TermPair { float t[3], l[3]; };
+  __device__ __attribute__((noinline)) static TermPair exact_terms(double g0, double g1, double g2, float eb0, float eb1,
+                                                                   float eb2, int m)
+  {
+    TermPair r;
+    const double g[3] = {g0, g1, g2};
+    const float eb[3] = {eb0, eb1, eb2};
+    for (int c = 0; c < 3; ++c)
+    {
+      float gmc = 1.0f, t = 0.0f, l = 0.0f;
+      for (int k = 1; k <= m; ++k)
+      {
+        l = t;
+        gmc = float(double(gmc) * (g[c] / double(k)));
+        t = float(exp(-g[c] - double(eb[c] / float(k))) * double(gmc) / double(k));
+      }
+      r.t[c] = t;
+      r.l[c] = l;
+    }
+    return r;
+  }
+
   // D (he.h:411-467), Eqs. 78-79: Taylor series in g with Beckmann's rough approximation blended in
   __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
   {
@@ -241,58 +265,63 @@ struct He
       for (int c = 0; c < 3; ++c)
       {
         const double rg = ddiv_nr(1.0, g[c]);    // g > APPROX here
-        rough[c] = float(double(exp_d2f(-double(eb[c]) * rg)) * rg);
+        rough[c] = float(exp_dd(-double(eb[c]) * rg) * rg);   // exp(-eb / g) / g in double, one rounding
       }
       weight = float(fmin(fmax(gmin - double(APPROX), 0.0), 1.0));
     }
     float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
     bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
-    // term = exp(-g - eb/m) g^m / m! / m, evaluated in double by the reference.  Split as exp(-g) (double, once
-    // per channel) x exp(-eb/m) (float argument eb/m exactly as the reference forms it, accurate float exp):
-    // the float-rounded term moves by an ulp or two, the series by ~1e-7 relative, and the loop body loses
-    // its double exp and divisions (the series is 3 x up to 64 terms per pair, the whole cost of this model)
+    // term = exp(-g - eb/m) gm / m in double by the reference, gm = float(gm * (g / m)) a float rounded per step
+    // (Spectrum *= array<double>), eb/m a float quotient.  gm and eb/m are formed exactly that way here; the
+    // exponential is split as exp(-g) (once per channel) x exp(-eb/m) (accurate float exp per term), so a term
+    // is within ~4 ulp of the reference's and the loop body has no double exp.  The series only runs for
+    // min(g) <= APPROX + 1, so g <= (APPROX + 1) (0.645 / 0.444)^2 < 45: exp(-g) stays a normal float.
     double eg[3];
-    float egf[3], gf[3];
+    float egf[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c)
     {
-      if (APPROX >= 0) egf[c] = converged ? 0.0f : exp_d2f(-g[c]);
+      if (APPROX >= 0) egf[c] = converged ? 0.0f : exp_d2f(-g[c]) * 1.15292150e+18f;   // x 2^60 (exact)
       else eg[c] = exp(-g[c]);
-      gf[c] = float(g[c]);
     }
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);
-      const float rmf = float(rm);
+      const float mf = float(m);
+      // exp(-eb/m) 2^60 (normal down to eb/m = 131: below that the term is < 2^-190 and rounds to 0 anyway) and
+      // exp(-g) 2^60: the products stay normal floats and one final scaling by 2^-120 rounds a term that is
+      // subnormal in the reference's double arithmetic once, as the reference's float(term) does
       float ex[3];
       if (WESTIN)
       {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) ex[c] = expf_neg(-(eb[c] * rmf));
+        for (int c = 0; c < 3; ++c) ex[c] = expf_scaled60(-div_small(eb[c], mf, float(rm)));
       }
-      else ex[0] = ex[1] = ex[2] = expf_neg(-(eb[0] * rmf));   // eb is the same for every channel
+      else ex[0] = ex[1] = ex[2] = expf_scaled60(-div_small(eb[0], mf, float(rm)));
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
         last[c] = term[c];
-        if (APPROX >= 0)
-        {
-          // the series only runs for min(g) <= APPROX + 1, so g <= (APPROX + 1) (0.645 / 0.444)^2 < 45: exp(-g),
-          // g^m / m! and their product stay normal floats and the products need no double
-          gm[c] = gm[c] * (gf[c] * rmf);
-          term[c] = (egf[c] * gm[c]) * (ex[c] * rmf);
-        }
-        else
-        {
-          gm[c] = float(double(gm[c]) * (g[c] * rm));
-          term[c] = float(eg[c] * double(ex[c]) * double(gm[c]) * rm);
-        }
+        gm[c] = float(double(gm[c]) * (g[c] * rm));
+        if (APPROX >= 0) term[c] = ((egf[c] * gm[c]) * (ex[c] * float(rm))) * 7.52316385e-37f;   // 2^-120
+        else term[c] = float(eg[c] * double(ex[c]) * double(gm[c]) * rm * 8.6736173798840355e-19);   // eg unscaled: 2^-60
         sum[c] += term[c];
       }
       if (ADAPTIVE)
       {
-        const float tmin = fminf(fminf(term[0], term[1]), term[2]);
-        const float lmin = fminf(fminf(last[0], last[1]), last[2]);
+        // converged |= hmin(term) < eps && hmin(term) < hmin(last) (he.h:460).  Near the series' peak the
+        // terms are nearly equal and a few-ulp difference would flip the test, truncating the sum one term
+        // early or late (a large relative change where D is tiny): where either comparison is within 1e-6,
+        // the decision is taken on the reference's exactly rounded terms m - 1 and m instead (terms below 2^-100 are
+        // rounded once from exact products already, see above).
+        float tmin = fminf(fminf(term[0], term[1]), term[2]);
+        float lmin = fminf(fminf(last[0], last[1]), last[2]);
+        if ((lmin >= 7.88860905e-31f && __builtin_fabsf(tmin - lmin) <= 1e-6f * lmin) || __builtin_fabsf(tmin - kEpsF) <= 1e-6f * kEpsF)
+        {
+          const TermPair x = exact_terms(g[0], g[1], g[2], eb[0], WESTIN ? eb[1] : eb[0], WESTIN ? eb[2] : eb[0], m);
+          tmin = fminf(fminf(x.t[0], x.t[1]), x.t[2]);
+          lmin = fminf(fminf(x.l[0], x.l[1]), x.l[2]);
+        }
         converged = (tmin < kEpsF) && (tmin < lmin);
       }
     }

@@ -505,7 +505,8 @@ int launch_reflectance(const ReflArgs& a, hipStream_t s)
 // ------------------------------------------------------------------------- fitting loss
 
 constexpr int kProbeBatch = 12;         // probes evaluated per pass over the samples (f64 accumulators)
-constexpr int kLossMaxBlocks = 2048;    // workspace = kLossMaxBlocks x nprobes doubles
+constexpr int kLossMaxBlocks = 2048;    // workspace = kLossMaxBlocks x nprobes doubles + the probes' models
+constexpr size_t kLossModelBytes = 512; // one constructed model per probe in the workspace
 
 struct LossArgs
 {
@@ -517,8 +518,25 @@ struct LossArgs
   int nprobes, stride, loss_kind;
   uint32_t component;
   double* block_sums;                   // [gridDim.x][nprobes]
+  char* models;                         // [nprobes][kLossModelBytes]: Model constructed once per probe
   double* sums;                         // [nprobes]
 };
+
+// One thread per probe: copy the probe's parameter vector into a zero-padded block (models that read slots
+// beyond their kParams -- He's and Merl's table pointers -- see zeros, never the next probe or past the
+// buffer), construct the Model once, and store it for k_loss, whose threads then read it with uniform loads
+// instead of re-running the constructor (tgamma, sampler setup, Aggregate weights) per sample and probe.
+template<class Model>
+__global__ __launch_bounds__(64) void k_loss_models(LossArgs a)
+{
+  const int p = blockIdx.x * 64 + threadIdx.x;
+  if (p >= a.nprobes) return;
+  ParamBlock q;
+#pragma unroll
+  for (int k = 0; k < kMaxParams; ++k) q.v[k] = (k < a.stride) ? a.probes[size_t(p) * size_t(a.stride) + k] : 0.0f;
+  const Model m(q.v);
+  __builtin_memcpy(a.models + size_t(p) * kLossModelBytes, &m, sizeof(Model));
+}
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -530,6 +548,7 @@ __device__ __forceinline__ double wave_sum(double v)
 template<class Model>
 __global__ __launch_bounds__(kBlock) void k_loss(LossArgs a)
 {
+  static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
   __shared__ double part[kBlock / 64][kProbeBatch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
@@ -553,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_loss(LossArgs a)
       for (int j = 0; j < kProbeBatch; ++j)
       {
         if (p0 + j >= a.nprobes) break;           // uniform
-        const Model m(a.probes + size_t(p0 + j) * size_t(a.stride));
+        const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(p0 + j) * kLossModelBytes);
         float rgb[3], pdf;
         m.template eval_pdf<kModeEval>(in, out, a.component, rgb, pdf);
         acc[j] += double(sample_loss(a.loss_kind, s, rgb));
@@ -588,6 +607,7 @@ int launch_loss(const LossArgs& a0, hipStream_t s)
   uint64_t blocks = (a.n + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
+  hipLaunchKernelGGL((k_loss_models<Model>), dim3(unsigned((a.nprobes + 63) / 64)), dim3(64), 0, s, a);
   hipLaunchKernelGGL((k_loss<Model>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   hipLaunchKernelGGL(k_loss_final, dim3(unsigned(a.nprobes)), dim3(kBlock), 0, s, a.block_sums, int(blocks), a.nprobes,
                      a.sums);

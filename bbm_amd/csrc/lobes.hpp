@@ -77,7 +77,7 @@ struct Ward
       if (KIND == 0) nf = kPi4F * sqrtf(in.z * out.z) * rx * ry;
       else if (KIND == 1) nf = kPi4F * rx * ry * (in.z * out.z);
       else nf = f_div_d(double(kPi4F * rx * ry) * (double(zH2) * double(zH2)), double(dot3(H, H)));
-      const float f = div_nr(expf(-exponent), nf);
+      const float f = div_nr(expf_dn(-exponent), nf);
       rgb[0] = active ? albedo[0] * f : 0.0f;
       rgb[1] = active ? albedo[1] * f : 0.0f;
       rgb[2] = active ? albedo[2] * f : 0.0f;
@@ -88,7 +88,7 @@ struct Ward
       const v3 h = halfway(in, out);
       const float nf = kPi4F * rx * ry * dot3(in, h) * cube_f(h.z);
       const float exponent = div_nr(sqnorm2(div_nr(h.x, rx), div_nr(h.y, ry)), h.z * h.z);
-      const float p = div_nr(expf(-exponent), nf);
+      const float p = div_nr(expf_dn(-exponent), nf);
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;
@@ -137,7 +137,7 @@ struct PhongLobe
   {
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
     const float cosA = fmaxf(dot3(mk3(-in.x, -in.y, in.z), out), 0.0f);
-    const float pw = powf(cosA, s);
+    const float pw = powf_fast(cosA, s);
     const float f = (s + 2) * kInvPiHalfF * pw;
     rgb[0] = active ? albedo[0] * f : 0.0f;
     rgb[1] = active ? albedo[1] * f : 0.0f;
@@ -193,7 +193,7 @@ struct Lafortune
     if (MODE & kModeEval)
     {
       const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
-      const float fr = powf(fmaxf(dot3(mk3(cx, cy, cz), mk3(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0f), s);
+      const float fr = powf_fast(fmaxf(dot3(mk3(cx, cy, cz), mk3(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0f), s);
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
@@ -208,7 +208,7 @@ struct Lafortune
       const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
       const v3 co = normalize3(mk3(cx * out.x, cy * out.y, cz * out.z));
       const float cosA = fmaxf(dot3(co, in), 0.0f);
-      const float p = div_nr(s + 1, kPi2F) * powf(cosA, s);
+      const float p = div_nr(s + 1, kPi2F) * powf_fast(cosA, s);
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;
@@ -314,7 +314,7 @@ struct AshikhminShirley
       exponent = su;
       normalization = f_div_d(double(su) + 1.0, double(kPi2F));
     }
-    const float p = div_nr(normalization * powf(h.z, exponent), 4.0f * hdi);
+    const float p = div_nr(normalization * powf_fast(h.z, exponent), 4.0f * hdi);
     return active ? p : 0.0f;
   }
 
@@ -342,12 +342,14 @@ struct AshikhminShirley
         exponent = su;
         normalization = div_nr(su + 1, kPi8F);
       }
-      const float np = normalization * powf(h.z, exponent);
+      const float np = normalization * powf_fast(h.z, exponent);
       float diff_scale = 0.0f;
       if constexpr (FULL)
       {
-        // hprod(1 - pow(1 - 0.5 (z_in, z_out), 5.0)) in double; 28 / (23 pi) in double
-        const double ai = 1.0 - 0.5 * in.z, ao = 1.0 - 0.5 * out.z;
+        // hprod(Scalar(1) - pow(Scalar(1) - 0.5 * Vec2d(z_in, z_out), 5.0)): `double * array<float>` is the
+        // array's friend operator*(const float&, array) (backbone/native/include/backbone/array.h:95), so
+        // 1 - 0.5 z is formed in float; pow(float, 5.0) and the rest are double; 28 / (23 pi) in double
+        const double ai = 1.0f - 0.5f * in.z, ao = 1.0f - 0.5f * out.z;
         const double ai2 = ai * ai, ao2 = ao * ao;
         const float scale = float((1.0 * (1.0 - ai2 * ai2 * ai)) * (1.0 - ao2 * ao2 * ao));
         const float normd = float(28.0 / (23.0 * double(kPiF)));
@@ -487,7 +489,7 @@ struct LowSmooth
     {
       const float dp2 = sqnorm2(in.x + out.x, in.y + out.y);
       const float cosD = float(safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y)));
-      const float S = powf_pos(float(1.0 + B * dp2), -C);     // double pow in the reference; see LowNdf::eval
+      const float S = powf_fast(float(1.0 + B * dp2), -C);     // double pow in the reference; see LowNdf::eval
       const float Q = fres.eval(cosD);
 #pragma unroll
       for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0f;

@@ -55,7 +55,7 @@ __device__ __forceinline__ v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
 // which returns the correctly rounded quotient except when n/d lies within ~2^-22 ulp of a
 // rounding midpoint (f32; ~2^-100 for the f64 form after two reciprocal refinements), i.e. a
 // 1-ulp difference in roughly one division in four million.  IEEE special cases (d = 0, d = inf,
-// n = inf, NaN) fall back to the uncorrected quotient, which is the IEEE result there.
+// n = inf, NaN) and subnormal quotients fall back to the uncorrected quotient, which is the IEEE result there.
 // Denormal divisors (|d| < 2^-126) are outside the domain of this path (directions are unit
 // vectors, parameters are >= their documented lower bounds).
 __device__ __forceinline__ float div_nr(float n, float d)
@@ -64,33 +64,161 @@ __device__ __forceinline__ float div_nr(float n, float d)
   const float q = n * r;
   const float e = __builtin_fmaf(-d, q, n);
   const float q1 = __builtin_fmaf(e, r, q);
-  return __builtin_isfinite(q1) ? q1 : q;
+  // q1 is the corrected quotient only where it is a normal float: for a subnormal quotient the remainder e is
+  // itself rounded to the subnormal grid and the "correction" can move a correctly rounded q (n * rcp(d), within
+  // ~1e-7 relative) off by an ulp; q is kept there, and for the IEEE special cases (inf, NaN, 0) as before.
+  return __builtin_isnormal(q1) ? q1 : q;
 }
 
-// exp(x) for a float x <= 0 to ~1 ulp without the library's range checks: x log2(e) split in a head (rounded
-// product) and tail (its fma residual + x times log2(e)'s own tail, one fused op), v_exp_f32 of the head, first-order fix-up
-// by the tail.  Results below the normal range flush to zero.
-__device__ __forceinline__ float expf_neg(float x)
+// ---------------------------------------------------------------- exponentials and powers
+//
+// Measured on gfx950 (tools/hwmath_probe.hip, every float in range): v_log_f32 is within 2.0 * 2^-24 relative of
+// log2(x) for all normal x (incl. x -> 1), v_exp_f32 within 1.42 * 2^-24 relative on [-1, 1].  Neither returns
+// subnormal results, and the device library's expf flushes below x = -103.28 although e^x still rounds to
+// 2^-149 down to x = -103.97.  The reference (glibc) rounds every result into the subnormal range, and a BSDF
+// value like D / (z_in z_out) carries such a subnormal into the normal range, so every exponential here
+// scales by 2^n with v_ldexp_f32 (one rounding, subnormals kept; the kernels run with f32 denormals enabled).
+constexpr float kLn2F = 0.693147180559945309f;
+
+// 2^f for |f| <= ~0.5 in double: Taylor series of e^(f ln2) to degree 11 (|f ln2| <= 0.347: remainder < 2^-44)
+__device__ __forceinline__ double exp2_poly(double f)
+{
+  const double u = f * 0.6931471805599453094;
+  double p = 2.505210838544171877e-08;                           // 1/11!
+  p = __builtin_fma(p, u, 2.755731922398589065e-07);
+  p = __builtin_fma(p, u, 2.755731922398589065e-06);
+  p = __builtin_fma(p, u, 2.480158730158730159e-05);
+  p = __builtin_fma(p, u, 1.984126984126984127e-04);
+  p = __builtin_fma(p, u, 1.388888888888888889e-03);
+  p = __builtin_fma(p, u, 8.333333333333333333e-03);
+  p = __builtin_fma(p, u, 4.166666666666666667e-02);
+  p = __builtin_fma(p, u, 1.666666666666666667e-01);
+  p = __builtin_fma(p, u, 0.5);
+  p = __builtin_fma(p, u, 1.0);
+  return __builtin_fma(p, u, 1.0);
+}
+
+// e^a in double for a in [-700, 700], to ~2^-44 relative (exp2_poly and an exact scaling)
+__device__ __forceinline__ double exp_dd(double a)
+{
+  const double t = a * 1.4426950408889634074;
+  const double n = __builtin_rint(t);
+  return __builtin_ldexp(exp2_poly(t - n), int(n));
+}
+
+// The float nearest 2^t for a double t: correctly rounded except within ~2^-18 ulp of a rounding midpoint
+// (2^-40 relative before the one rounding), over the whole range: overflow to inf, subnormal results rounded
+// once by the f64 -> f32 conversion (f32 denormals are enabled), 0 below 2^-150.
+__device__ __forceinline__ float exp2_cr(double t)
+{
+  const double n = __builtin_rint(t);
+  const double p = exp2_poly(t - n);
+  const float r = float(__builtin_ldexp(p, int(__builtin_fmin(__builtin_fmax(n, -400.0), 400.0))));
+  return (t < -400.0) ? 0.0f : ((t > 400.0) ? __builtin_inff() : r);   // +-inf; NaN propagates through r
+}
+
+// expf over the whole float range to ~1.5 ulp (normal results: x log2(e) split into a head and a tail, v_exp_f32
+// of the fraction, v_ldexp_f32 by the integer part -- the library's scheme); results in the subnormal range
+// (x < -87.34) are rounded once from exp2_cr, as the reference's glibc expf rounds them.
+__device__ __forceinline__ float expf_dn(float x)
 {
   constexpr float kLog2eHi = 1.44269502162933349609375f;          // float(log2 e)
   constexpr float kLog2eLo = 1.925963033500011079e-08f;          // log2 e - kLog2eHi
-  constexpr float kLn2 = 0.693147180559945309f;
+  if (__builtin_expect(x < -87.33f, 0))
+  {
+    if (x < -104.0f) return 0.0f;                                // e^x < 2^-150 (x = -inf included)
+    return exp2_cr(double(x) * 1.4426950408889634074);
+  }
   const float t = x * kLog2eHi;
   const float e = __builtin_fmaf(x, kLog2eLo, __builtin_fmaf(x, kLog2eHi, -t));
-  const float r = __builtin_amdgcn_exp2f(t);
-  return __builtin_fmaf(r, e * kLn2, r);
+  const float n = __builtin_rintf(t);
+  const float r = __builtin_ldexpf(__builtin_amdgcn_exp2f((t - n) + e), int(n));
+  return (x > 88.7228394f) ? __builtin_inff() : r;                 // NaN propagates through r
 }
 
-// float(exp(a)) for a double argument, to ~1 ulp of the float result: a log2(e) in double, split into a float
-// head and tail, v_exp_f32 of the head, first-order fix-up by the tail (a handful of f64 ops instead of a full
-// double exp).  +-inf and overflow give inf / 0 like the reference; results below the normal range flush.
+// e^x 2^60 for a finite float x <= 0 (the He series' terms): ~1.5 ulp while the result is a normal float
+// (x >= -131.6), rounded into the subnormal range by v_ldexp_f32 below that and 0 below x = -150
+__device__ __forceinline__ float expf_scaled60(float x)
+{
+  constexpr float kLog2eHi = 1.44269502162933349609375f;
+  constexpr float kLog2eLo = 1.925963033500011079e-08f;
+  const float t = x * kLog2eHi;
+  const float e = __builtin_fmaf(x, kLog2eLo, __builtin_fmaf(x, kLog2eHi, -t));
+  const float n = __builtin_rintf(t);
+  return __builtin_ldexpf(__builtin_amdgcn_exp2f((t - n) + e), int(n) + 60);
+}
+
+// a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
+// q = a rm corrected once by the exact remainder -- the correctly rounded quotient (as div_nr) without v_rcp_f32
+__device__ __forceinline__ float div_small(float a, float m, float rm)
+{
+  const float q = a * rm;
+  return __builtin_fmaf(__builtin_fmaf(-m, q, a), rm, q);
+}
+
+// expf to ~0.5 ulp (correctly rounded but within ~2^-18 ulp of a midpoint): for the few places where the
+// result is cancelled against a constant right after (Bagher's 1 - e^(c theta^k)), so the reference's
+// correctly rounded glibc expf must be reproduced, not approximated
+__device__ __forceinline__ float expf_acc(float x)
+{
+  if (__builtin_fabsf(x) < 1.49011612e-08f) return 1.0f;     // |x| < 2^-26: e^x rounds to 1
+  return exp2_cr(double(x) * 1.4426950408889634074);
+}
+
+// float(exp(a)) for a double argument, to ~1.5 ulp of the float result: a log2(e) in double, split into an
+// integer, a float head and a float tail, v_exp_f32 of the head, first-order fix-up by the tail, ldexp by the
+// integer (a handful of f64 ops instead of a full double exp).  +-inf and overflow give inf / 0 like the
+// reference; results in the subnormal range come from exp2_cr (one rounding).
 __device__ __forceinline__ float exp_d2f(double a)
 {
   const double t = a * 1.4426950408889634074;
-  const float th = float(t);
-  const float tl = float(t - double(th));
-  const float r = __builtin_amdgcn_exp2f(th);
-  return __builtin_isinf(th) ? r : __builtin_fmaf(r, tl * 0.693147180559945309f, r);
+  if (t < -126.0) return exp2_cr(t);
+  const double n = __builtin_rint(t);
+  const double f = t - n;
+  const float fh = float(f);
+  const float fl = float(f - double(fh));
+  const float r0 = __builtin_amdgcn_exp2f(fh);
+  const float r = __builtin_ldexpf(__builtin_fmaf(r0, fl * kLn2F, r0), int(__builtin_fmin(n, 400.0)));
+  return (t > 200.0) ? __builtin_inff() : r;   // NaN propagates through r
+}
+
+// log2(x) for a normal or subnormal float x > 0 to ~2^-44 absolute (+ 2^-52 relative), in double:
+// l0 = v_log_f32(x) (2 * 2^-24 relative), then one Newton step on 2^L = x with 2^-l0 from exp2_poly:
+// q = x 2^-l0 = 1 + e (|e| < 2^-16), L = l0 + log2(1 + e) with e - e^2/2 + e^3/3.
+__device__ __forceinline__ double log2_acc(float x)
+{
+  const bool sub = x < 1.17549435e-38f;
+  const float xs = sub ? x * 4294967296.0f : x;                 // 2^32: v_log_f32 needs a normal input
+  const float l0 = __builtin_amdgcn_logf(xs);
+  const float n = __builtin_rintf(l0);
+  const double p = exp2_poly(-double(l0 - n));                   // 2^-(l0 - n), l0 - n exact
+  const double e = __builtin_fma(double(xs), __builtin_ldexp(p, -int(n)), -1.0);
+  const double l1p = e * __builtin_fma(e, __builtin_fma(e, 1.0 / 3.0, -0.5), 1.0);
+  return (double(l0) + l1p * 1.4426950408889634074) - (sub ? 32.0 : 0.0);
+}
+
+// x^y where the result is used as a factor (not amplified by an exponential or a cancellation): on the
+// transcendental unit, exp2(y v_log_f32(x)), where |y log2 x| <= 8 -- relative error <= ln2 8 3.6e-7 / 2 + 1.4 ulp
+// = 1.1e-6, results in [2^-8, 2^8] -- and powf_acc elsewhere.
+__device__ __forceinline__ float powf_acc(float x, float y);
+__device__ __forceinline__ float powf_fast(float x, float y)
+{
+  const float t0 = y * __builtin_amdgcn_logf(x);
+  if (__builtin_fabsf(t0) <= 8.0f && x >= 1.17549435e-38f) return __builtin_amdgcn_exp2f(t0);
+  return powf_acc(x, y);
+}
+
+// x^y for x >= 0 (or NaN), y finite: the float nearest exp2(y log2 x) with y log2 x formed in double to ~2^-40,
+// i.e. the correctly rounded power except within ~2^-18 ulp of a midpoint, over the whole float range
+// (subnormal results included) -- what the reference's glibc powf / double pow rounded to float return.
+// ~40 VALU (v_log_f32 + two short f64 polynomials) against 173 for the device library's powf.
+__device__ __forceinline__ float powf_acc(float x, float y)
+{
+  float r = exp2_cr(double(y) * log2_acc(x));
+  // pow(x, 0) = 1 (x NaN included); pow(0, y) = 0 / inf; x < 0 is outside the domain (NaN)
+  r = (x == 0.0f) ? ((y > 0.0f) ? 0.0f : __builtin_inff()) : r;
+  r = (x < 0.0f) ? __builtin_nanf("") : r;
+  return (y == 0.0f) ? 1.0f : r;
 }
 
 // 1 / m for the loop counters of the series kernels (m <= 64), a uniform scalar load instead of a division
@@ -154,7 +282,7 @@ __device__ __forceinline__ float div_ff(float nh, float nl, float dh, float dl)
   q = __builtin_fmaf(__builtin_fmaf(-dh, q, nh), r, q);           // ~correctly rounded nh / dh
   const float rem = __builtin_fmaf(-dh, q, nh) + __builtin_fmaf(-q, dl, nl);
   const float q1 = __builtin_fmaf(rem, r, q);
-  return __builtin_isfinite(q1) ? q1 : nh * r;
+  return __builtin_isnormal(q1) ? q1 : nh * r;     // subnormal / special results: see div_nr
 }
 
 // horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2
@@ -249,11 +377,6 @@ __device__ __forceinline__ float powf_xlog(float x, float y)
 {
   return (x > 0.0f) ? float(exp(double(y) * log(double(x)))) : 0.0f;
 }
-// x^y for x > 0 on the transcendental unit: exp2(y log2 x), v_log_f32 + v_exp_f32 (each ~1 ulp).
-// Relative error ~ (1 + |y log2 x|) * 2^-23: below 3e-6 wherever the result is a normal float that
-// matters (|y log2 x| < 25), vs ~100 VALU instructions for the library powf.  x <= 0 gives NaN / 0 / inf
-// like exp2(y * log2(x)); callers select those lanes away.
-__device__ __forceinline__ float powf_pos(float x, float y) { return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x)); }
 // glibc powf (what std::pow(float, float) calls) is computed in double and rounded once; so is this
 __device__ __forceinline__ float powf_cr(float x, float y) { return float(pow(double(x), double(y))); }
 

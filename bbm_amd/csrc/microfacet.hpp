@@ -28,7 +28,7 @@ struct Beckmann
   {
     const float c2 = h.z * h.z;
     const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
-    float D = div_nr(expf(div_nr(-sn, c2)), au * av * c2 * c2);
+    float D = div_nr(expf_dn(div_nr(-sn, c2)), au * av * c2 * c2);
     if (Normalize) D *= kInvPiF;
     return (h.z > 0) ? D : 0.0f;
   }
@@ -56,11 +56,11 @@ struct Beckmann
     float xc0 = clampf(xi0, float(10e-6), float(1.0 - 10e-6));
     const float xc1 = clampf(xi1, float(10e-6), float(1.0 - 10e-6));
     float x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
-    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf(-(vs.z * vs.z))));
+    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_dn(-(vs.z * vs.z))));
     for (int i = 0; i < 3; ++i)
     {
       const float slope = float(erfinv_d(x));
-      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf(-slope * slope) - xc0);
+      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_dn(-slope * slope) - xc0);
       const float der = float(1.0 - slope * tanT);
       x -= div_nr(val, der);
     }
@@ -139,7 +139,7 @@ struct PhongNdf
   __device__ __forceinline__ float eval(v3 h) const
   {
     const float normalization = div_nr(sharpness + 2, float(2.0f * kPiD));
-    const float D = powf_pos(h.z, sharpness) * normalization;   // h.z <= 0 lanes are selected away
+    const float D = powf_fast(h.z, sharpness) * normalization;   // h.z <= 0 lanes are selected away
     return (h.z > 0) ? D : 0.0f;
   }
   __device__ __forceinline__ float G1(v3 v, v3 m) const
@@ -176,7 +176,7 @@ struct StudentT
   __device__ explicit StudentT(const float* p) : au(p[0]), av(Aniso ? p[1] : p[0]), gamma(p[Aniso ? 2 : 1])
   {
     lam_scale = tgamma(gamma - 0.5) / double(tgammaf(gamma)) * kInvSqrtPiF;
-    s1_scale = div_nr(powf(gamma - 1, gamma), 2 * gamma - 3);
+    s1_scale = div_nr(powf_cr(gamma - 1, gamma), 2 * gamma - 3);
     sqrt_g1 = sqrtf(gamma - 1);
     f22 = F22(gamma);
     f23 = F23(gamma);
@@ -188,10 +188,10 @@ struct StudentT
     const float z2 = h.z * h.z;
     const float normalization = kPiF * alpha2 * (z2 * z2);       // pow(cos, 4): powf(x, 4) = (x^2)^2 exactly rounded here
     const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
-    // pow(1 + tan^2 / ((gamma - 1) alpha^2), gamma): the reference rounds a double pow; exp2(gamma log2 x)
-    // on the transcendental unit is within (1 + gamma log2 x) 2^-23 of it -- below 3e-6 wherever D is
-    // within 1e-6 of its peak (156 f64 instructions saved per pair)
-    const float den = powf_pos(float(1.0 + div_nr(sn, (gamma - 1) * pow2f(h.z))), gamma);
+    // pow(1 + tan^2 / ((gamma - 1) alpha^2), gamma): the reference rounds a double pow; powf_fast is within
+    // ~1e-6 of it (the transcendental unit where |gamma log2 x| <= 8, a double exponent beyond) instead of 227
+    // f64 instructions
+    const float den = powf_fast(float(1.0 + div_nr(sn, (gamma - 1) * pow2f(h.z))), gamma);
     const float D = div_nr(1.0f, normalization * den);
     return (h.z > 0) ? D : 0.0f;
   }
@@ -225,9 +225,8 @@ struct StudentT
     const bool mask = (v.z > 0) && (dot3(v, m) > 0);
     const bool normal_mask = v.z < 1.0 - kEpsF;
     const float z = v.z * div_nr(1.0f, sqrtf(sqnorm2(v.x * au, v.y * av)));
-    // S1 = pow((gamma - 1) + z^2, 3/2 - gamma) / z (double in the reference): G1 = 1 / (1 + lambda) is
-    // well conditioned in S1 (near the normal lambda -> 0 and G1 -> 1), so the f32 pow suffices
-    const float S1 = div_nr(powf_pos((gamma - 1) + z * z, float(3.0 / 2.0 - gamma)), z);
+    // S1 = pow((gamma - 1) + z^2, 3/2 - gamma) / z (double in the reference), ~1e-6 via powf_fast
+    const float S1 = div_nr(powf_fast((gamma - 1) + z * z, float(3.0 / 2.0 - gamma)), z);
     const float S2 = F21(z) * (f22 + f23 * F24(z));
     const double lam = lam_scale * double(s1_scale * S1 + sqrt_g1 * S2) - 0.5;
     const float lambda = normal_mask ? float(lam) : 0.0f;
@@ -344,8 +343,8 @@ struct LowNdf
 
   __device__ __forceinline__ float eval(v3 h) const
   {
-    // pow(1 + B (1 - z), -C) in double in the reference; f32 exp2(-C log2 x): ~(1 + C log2 x) 2^-23
-    const float S = powf_pos(float(1.0 + B * (1.0 - h.z)), -C);
+    // pow(1 + B (1 - z), -C) in double in the reference; powf_fast: within ~1e-6
+    const float S = powf_fast(float(1.0 + B * (1.0 - h.z)), -C);
     return (h.z > 0) ? S : 0.0f;
   }
 
@@ -433,7 +432,8 @@ __device__ __forceinline__ float eval_scale(float x, float y)
     dl = __builtin_fmaf(y, kPiLo, dl);
     return div_ff(x, 0.0f, dh, dl);
   }
-  return div_nr(N == Norm::Walter ? x * 0.25f : x, y);
+  // Walter: (x / 4.0) / y in double = x / (4 y), 4 y exact in float (x * 0.25f would round a subnormal x)
+  return div_nr(x, N == Norm::Walter ? 4.0f * y : y);
 }
 
 template<class NDF, class MS, class FRESNEL, Norm N, bool Scaled>

@@ -56,7 +56,7 @@ struct Bagher
     // k ~ 48, c ~ 1e-7 -> g ~ 5e-4 at grazing angles): pow and theta must round like the reference's
     // (pow rounded from f64 exp(k log d), which is the correctly rounded powf; powf_xlog's domain holds: d > 0 where
     // the result is used, and the fit bounds keep k > 0)
-    const float g = 1.0f + Lambda[j] * (1.0f - expf(c[j] * powf_xlog(th - theta0[j], k[j])));
+    const float g = 1.0f + Lambda[j] * (1.0f - expf_acc(c[j] * powf_xlog(th - theta0[j], k[j])));
     return (th > theta0[j]) ? g : 1.0f;
   }
 
@@ -83,10 +83,9 @@ struct Bagher
       {
         // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
         const float t = alpha[j] + div_nr(tan2, alpha[j]);
-        // exp(-t) / t^p is well conditioned: exp2(p log2 t) on the transcendental unit (relative error
-        // ~(1 + |p log2 t|) 2^-23) instead of the 173-instruction library powf
-        const float den = powf_pos(t, p[j]);
-        const float P22 = (den > kEpsF) ? div_nr(expf(-t), den) : 0.0f;
+        // exp(-t) / t^p: powf_fast (~1e-6) instead of the 173-instruction library powf
+        const float den = powf_fast(t, p[j]);
+        const float P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
         const float Dj = ((h.z > 0) ? f_div_d(double(P22), dnorm) : 0.0f) * K[j];
         const float Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0f;
         // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos

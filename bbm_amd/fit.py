@@ -25,7 +25,7 @@ import math
 import numpy as np
 
 from . import _lib
-from .backbone import _stream_ptr, _torch
+from .backbone import _on_stream, _stream_ptr, _torch
 
 LIN_SPHERICAL, LIN_MERL = 0, 1
 NGAN_L2, LOW_L2, BIERON_L2, STANDARD_LOG, LOW_LOG, BIERON_LOG = range(6)
@@ -153,6 +153,11 @@ class SampledLoss:
         cross-rank all-reduce -- RCCL over xGMI, 2P doubles per compass step."""
         sums = self.local_sums(probes)
         if self.dist is not None and self.dist.get_world_size() > 1:
+            torch = _torch()
+            stream = getattr(self, "stream", None)
+            if stream is not None and sums.is_cuda:
+                # the collective runs on the current stream: order it after the loss launch on self.stream
+                torch.cuda.current_stream().wait_stream(stream)
             self.dist.all_reduce(sums)
         return sums
 
@@ -164,6 +169,7 @@ class SampledLoss:
         dp = torch.from_numpy(p).to(self.dev, non_blocking=False)
         sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
         ws = self._workspace(nprobes)
+        _on_stream(self.stream, dp, sums, ws)
         lib = _lib.load()
         if self.pairs is not None:
             din, dout = self.pairs

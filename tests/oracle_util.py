@@ -100,6 +100,21 @@ def ref_sample(name, params, dout, xi, component=3, unit=0, nthreads=1):
     return _sample(lib.bbmref_sample, name, params, dout, xi, component, unit, nthreads)
 
 
+def ref_reflectance(name, params, dout, component=3, unit=0):
+    """(3, N): reflectance(out) from the reference itself."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n = dout.shape[1]
+    res = np.zeros((3, n), np.float32)
+    rc = lib.bbmref_reflectance(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(dout[0]),
+                                _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component), ctypes.c_uint32(unit),
+                                _fp(res[0]), _fp(res[1]), _fp(res[2]))
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return res
+
+
 def oracle_models():
     """Models a CPU checker can evaluate on arbitrary inputs: the reference shim if it is present
     (prebuilt in the build container, travels with the tree), else the C restatement."""
@@ -161,21 +176,146 @@ def ulp_diff(got, ref):
     return d
 
 
-# Parity bar (BASELINE.json north_star): |gpu - ref| <= 1e-5 |ref|, with an absolute floor of
-# 1e-6 x max|ref| over the batch for outputs that are ~1e-6 of the batch peak or smaller (values
-# deep in an exponential tail, where one ulp of the exp argument is amplified).
+# Parity bar (BASELINE.json north_star), lane by lane, no batch-dependent floor:
+#   * every lane whose reference value is a normal float (|ref| >= FLT_MIN):  |gpu - ref| <= 1e-5 |ref|;
+#   * lanes whose reference value is subnormal or zero: |gpu - ref| <= 1e-5 FLT_MIN (the same bar, continued
+#     below the normal range with the absolute step it has at FLT_MIN: ~83 subnormal ulps);
+#   * NaN where the reference is NaN, the same infinity where it is infinite.
+# Nothing else is excused here; a test that accepts a lane outside this bar must prove that lane on its own
+# (e.g. the reference, given inputs a few ulps away, reproduces the GPU value: test_gpu_parity.py).
 REL_TOL = 1e-5
-ABS_FLOOR_FRAC = 1e-6
+FLT_MIN = float(np.finfo(np.float32).tiny)
 
 
-def parity_violations(got, ref, rel_tol=REL_TOL, abs_floor_frac=ABS_FLOOR_FRAC):
+def parity_ok(got, ref, rel_tol=REL_TOL):
+    """Boolean mask of lanes that meet the bar above."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
-    finite = np.isfinite(ref)
-    peak = np.max(np.abs(ref[finite])) if finite.any() else 0.0
-    tol = rel_tol * np.abs(ref) + abs_floor_frac * peak
-    ok = (np.abs(got - ref) <= tol) | (got == ref) | (np.isnan(got) & np.isnan(ref))
-    return np.nonzero(~ok)
+    with np.errstate(invalid="ignore"):
+        tol = rel_tol * np.maximum(np.abs(ref), FLT_MIN)
+        ok = (np.abs(got - ref) <= tol) | (got == ref) | (np.isnan(got) & np.isnan(ref))
+    return ok
+
+
+def parity_violations(got, ref, rel_tol=REL_TOL):
+    return np.nonzero(~parity_ok(got, ref, rel_tol))
+
+
+def perturb_ulps(a, steps):
+    """a (float32) moved by `steps` (integer array, same shape) float steps: the float `steps` positions away in
+    the ordered float line (np.nextafter applied |steps| times, vectorised on the bit patterns)."""
+    a = np.asarray(a, np.float32)
+    b = a.view(np.int32).astype(np.int64)
+    key = np.where(b < 0, -(b & 0x7FFFFFFF), b) + np.asarray(steps, np.int64)
+    out = np.where(key < 0, (-key) | 0x80000000, key).astype(np.uint32).view(np.float32)
+    return out
+
+
+def explained_by_input_ulps(ref_fn, inputs, got, k=2, trials=48, seed=1234):
+    """Per-lane proof for lanes outside the bar (backward error): True for a lane where every output channel of
+    the GPU lies within the bar of -- or between -- the reference's own outputs at inputs whose coordinates are
+    each moved by at most k float steps (the unmoved input and `trials - 1` random moves, seeded).  Such a lane's
+    difference is the reference's own sensitivity to the last bits of its input (subnormal intermediates,
+    cancellation), not a different computation.
+      ref_fn(*inputs) -> (c, n) reference outputs; inputs: list of (k_i, n) float32 arrays (directions, xi);
+      got: (c, n) GPU outputs of the lanes to prove."""
+    inputs = [np.asarray(a, np.float32) for a in inputs]
+    got = np.asarray(got, np.float64)
+    n = got.shape[1]
+    if n == 0:
+        return np.zeros(0, bool)
+    rng = np.random.default_rng(seed)
+    moved = []
+    for a in inputs:
+        st = rng.integers(-k, k + 1, size=(trials,) + a.shape)
+        st[0] = 0
+        moved.append(np.concatenate([perturb_ulps(a, st[t]) for t in range(trials)], axis=1))
+    r = np.asarray(ref_fn(*moved), np.float64).reshape(got.shape[0], trials, n)
+    with np.errstate(invalid="ignore"):
+        lo = np.nanmin(r, axis=1)
+        hi = np.nanmax(r, axis=1)
+        tol = REL_TOL * np.maximum(np.maximum(np.abs(lo), np.abs(hi)), FLT_MIN)
+        ok = ((got >= lo - tol) & (got <= hi + tol)) | (np.isnan(got) & np.isnan(r).any(axis=1))
+    return ok.all(axis=0)
+
+
+# ----------------------------------------------------------------- data-driven sampler pdf (He family, Merl)
+#
+# ndf_sampler's pdf (bbm/ndf_sampler.h:128-156 -> ndf/sampler.h:102-128) is a lookup in a 90-bin CDF built from
+# the model's own backscatter evaluations (ndf/sampler.h:143-181, util/cdf.h:39-47).  A CDF entry is a running
+# float sum normalised by the total, and a bin's pdf is the difference of two adjacent entries: one ulp in an
+# entry near 1 is ~1e-5 of a small bin.  So a 1-ulp difference in a single backscatter evaluation (well inside
+# the eval bar) moves the pdf of every direction in the neighbouring bins by up to ~2e-5.  The functions below
+# restate that arithmetic in numpy float32 (checked against the reference's own pdf in tests/test_gpu_parity.py)
+# so a pdf lane outside the bar can be proven: the GPU value is what the reference's pdf arithmetic gives on the
+# CDF built from the GPU's backscatter evaluations, and those evaluations meet the eval bar.
+
+SAMPLER_BINS = 90
+
+
+def sampler_backscatter_dirs():
+    """The 90 halfway vectors h_i at theta = (i/90)^2 pi/2, phi = 0 (ndf/sampler.h:157-166), as (3, 90)."""
+    f = np.float32
+    q = (np.arange(SAMPLER_BINS, dtype=f) / f(SAMPLER_BINS)).astype(f)
+    th = (q.astype(np.float64) ** 2 * np.float64(f(0.5 * np.pi))).astype(f)
+    return np.stack([np.sin(th.astype(np.float64)), np.zeros(SAMPLER_BINS),
+                     np.cos(th.astype(np.float64))]).astype(f)
+
+
+def sampler_cdf(backscatter_rgb):
+    """util/cdf.h:39-47 over samples hsum(eval(h_i, h_i)) sin(theta1) sqrt(theta1), theta1 = ((i+1)/90)^2 pi/2."""
+    f = np.float32
+    rgb = np.asarray(backscatter_rgb, f)
+    hs = ((f(0) + rgb[0]) + rgb[1]) + rgb[2]
+    q1 = (np.arange(1, SAMPLER_BINS + 1, dtype=f) / f(SAMPLER_BINS)).astype(f)
+    th1 = (q1.astype(np.float64) ** 2 * np.float64(f(0.5 * np.pi))).astype(f)
+    w = (np.sin(th1.astype(np.float64)).astype(f) * np.sqrt(th1)).astype(f)
+    acc = np.cumsum((hs * w).astype(f), dtype=f)
+    return (acc / acc[-1]).astype(f)
+
+
+def sampler_pdf(cdf, din, dout):
+    """ndf_sampler::pdf(in, out) for component/unit whose CDF is `cdf` (float32 arithmetic as the reference)."""
+    f = np.float32
+    din = np.asarray(din, f)
+    dout = np.asarray(dout, f)
+    cdf = np.asarray(cdf, f)
+    hx, hy, hz = din[0] + dout[0], din[1] + dout[1], din[2] + dout[2]
+    inv = (f(1) / np.sqrt(((f(0) + hx * hx) + hy * hy) + hz * hz)).astype(f)
+    h = np.stack([hx * inv, hy * inv, hz * inv]).astype(f)
+    sz = np.where(h[2] < 0, f(-1), f(1)).astype(f)
+    dz = (h[2] - sz).astype(f)
+    nrm = np.sqrt(((f(0) + h[0] * h[0]) + h[1] * h[1]) + dz * dz).astype(f)
+    t = 2.0 * np.arcsin(0.5 * nrm.astype(np.float64))
+    theta = np.where(h[2] >= 0, t, np.float64(f(np.pi)) - t).astype(f)
+    ti = ((np.sqrt(theta / f(0.5 * np.pi)) * f(SAMPLER_BINS)).astype(np.float64) - 0.5).astype(f)
+    fl, ce = np.floor(ti), np.ceil(ti)
+    w = (ti - fl).astype(f)
+    lidx = np.where(fl < 0, SAMPLER_BINS - 1, np.minimum(fl, SAMPLER_BINS - 1)).astype(np.int64)
+    uidx = np.where(ce < 0, SAMPLER_BINS - 1, np.minimum(ce, SAMPLER_BINS - 1)).astype(np.int64)
+    prev = np.concatenate([[f(0)], cdf[:-1]]).astype(f)
+    cp = (cdf - prev).astype(f)
+    p = (cp[lidx] * (f(1) - w) + cp[uidx] * w).astype(f)
+    st = np.sin(theta.astype(np.float64)).astype(f)
+    jac = ((((np.sqrt(theta) * f(f(0.25 * np.pi) * f(np.pi))) / f(SAMPLER_BINS)) * np.abs(st)) * f(2 * np.pi)).astype(f)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ph = np.where((h[2] > 0) & (jac > np.finfo(f).eps), p / jac, f(0)).astype(f)
+        oh = ((f(0) + dout[0] * h[0]) + dout[1] * h[1]) + dout[2] * h[2]
+        pdf = (ph.astype(np.float64) / np.abs(4.0 * oh.astype(np.float64))).astype(f)
+    return np.where((dout[2] > 0) & (din[2] > 0), pdf, f(0))
+
+
+def max_rel_normal(got, ref):
+    """max |gpu - ref| / |ref| over the lanes with a normal (|ref| >= FLT_MIN) finite reference value."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    sel = np.isfinite(ref) & (np.abs(ref) >= FLT_MIN)
+    if not sel.any():
+        return 0.0
+    with np.errstate(invalid="ignore"):
+        r = np.abs(got[sel] - ref[sel]) / np.abs(ref[sel])
+    r[np.isnan(r)] = np.inf
+    return float(r.max())
 
 
 # ------------------------------------------------------------------------------ directions

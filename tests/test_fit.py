@@ -137,7 +137,19 @@ def test_sharded_compass_two_ranks_gloo():
     procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = {}
+    import queue
+    import time
+    t0 = time.time()
+    while len(res) < len(procs):
+        try:
+            r, v = q.get(timeout=2)
+            res[r] = v
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a rank died (exit codes {dead})"
+            assert time.time() - t0 < 300, "ranks did not finish"
+
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

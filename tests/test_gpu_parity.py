@@ -2,11 +2,23 @@
 
 Every check goes through the C-ABI (libbbm_hip via bbm_amd) and is compared with
   * the reference's own outputs (tests/golden, floatRGB, written by oracle/gen_golden.py), and
-  * the C restatement (oracle/port) on fresh seeded batches, including sizes far beyond the
-    fixtures (size-independent properties: eval+pdf == eval, pdf separately; masks; tails).
-Tolerance (north_star): |gpu - ref| <= 1e-5 |ref| + 1e-6 max|ref| (see oracle_util.parity_violations);
-in practice the kernels agree to a few ulp, and the max ulp distance is reported.
+  * the reference itself (oracle/_ref, prebuilt) on fresh seeded batches of 1M pairs.
+
+The bar (BASELINE.json north_star: <= 1e-5 relative) is applied lane by lane, with no batch-dependent floor
+(tests/oracle_util.parity_ok): |gpu - ref| <= 1e-5 |ref| for every normal reference value, the same absolute
+step (1e-5 FLT_MIN) below the normal range, NaN for NaN.  A lane outside the bar fails unless it is proven on
+its own, by one of two per-lane arguments, and the number of such lanes is reported and bounded:
+  * input ulps (backward error): the reference itself, at inputs moved by <= 2 float steps per coordinate,
+    produces values on both sides of the GPU's (oracle_util.explained_by_input_ulps) -- the lane's difference
+    is the reference's own sensitivity to the last bits of its input (subnormal intermediates, cancellation);
+  * sampler CDF (the data-driven samplers of the He family): the GPU pdf is what the reference's pdf
+    arithmetic gives on the CDF built from the GPU's backscatter evaluations, and those evaluations meet the
+    bar (oracle_util.sampler_cdf / sampler_pdf): a 1-ulp difference in one of the 90 evaluations moves the
+    pdf of the neighbouring bins by up to ~2e-5 through the CDF's differences.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -17,6 +29,8 @@ pytestmark = pytest.mark.gpu
 
 META = ou.golden_meta()
 INP = ou.golden_inputs()
+TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
+MAX_EXCUSED_FRAC = 1e-3       # at most this fraction of a batch's lanes may need a per-lane proof
 
 
 @pytest.fixture(scope="module")
@@ -37,70 +51,13 @@ def _gpu_evalpdf(model, din, dout, **kw):
     return np.concatenate([rgb.cpu().numpy(), pdf.cpu().numpy()[None]], 0)
 
 
-def _assert_parity(got, ref, what):
-    bad = ou.parity_violations(got, ref)
-    assert len(bad[0]) == 0, (f"{what}: {len(bad[0])} values outside tolerance; e.g. got "
-                              f"{got[bad][:5]} ref {ref[bad][:5]}")
-    assert np.array_equal(np.isnan(got), np.isnan(ref)), f"{what}: NaN pattern differs"
-    # lanes the reference returns exactly 0 for (masked, below horizon, ...) are 0 here too,
-    # except values deep in an underflowing tail (below the absolute floor)
-    finite = np.isfinite(ref)
-    floor = ou.ABS_FLOOR_FRAC * (np.abs(ref[finite]).max() if finite.any() else 0.0)
-    stray = (ref == 0) & (np.abs(got) > floor)
-    assert not stray.any(), f"{what}: {stray.sum()} lanes non-zero where the reference is 0"
-    return _stats(got, ref, floor)
-
-
-def _pdf_at_dir(name, params, dirs, outs, xi, flags):
-    """The pdf the reference's sampler would report for a sample at `dirs`.  For every model but
-    one that is pdf(dir, out).  AshikhminShirleyFull's one-sample mixture
-    (ashikhminshirleyfull.h:96-124) draws a specular candidate with xi0 / w_s and a diffuse one
-    with (xi0 - w_s) / w_d (0 when w_d <= eps), returns the one selected by xi0 <= w_s, and
-    reports w_s pdf_s(specular candidate) + w_d pdf_d(diffuse candidate): the chosen candidate's
-    pdf is taken at the GPU direction, the other candidate is drawn by the reference itself."""
-    if name != "AshikhminShirleyFull":
-        return ou.oracle_eval_pdf(name, params, dirs, outs, nthreads=8)[3]
-    p = np.asarray(params, np.float32)
-    one, eps = np.float32(1), np.finfo(np.float32).eps
-    spec_albedo = (p[3] + p[4]) + p[5]
-    diff_albedo = ((p[0] + p[1]) + p[2]) * (one - spec_albedo)
-    dw = diff_albedo / (diff_albedo + spec_albedo)
-    sw = one - dw
-    xi = np.asarray(xi, np.float32)
-    xs = np.stack([xi[0] / sw if sw > eps else np.zeros_like(xi[0]), xi[1]])
-    xd = np.stack([(xi[0] - sw) / dw if dw > eps else np.zeros_like(xi[0]), xi[1]])
-    flags = np.asarray(flags)
-    ps = np.where(flags == 2, ou.oracle_eval_pdf(name, params, dirs, outs, component=2, nthreads=8)[3],
-                  ou.oracle_sample(name, params, outs, xs, component=2, nthreads=8)[0][3])
-    pd = np.where(flags == 1, ou.oracle_eval_pdf(name, params, dirs, outs, component=1, nthreads=8)[3],
-                  ou.oracle_sample(name, params, outs, xd, component=1, nthreads=8)[0][3])
-    return (sw * ps.astype(np.float32) + dw * pd.astype(np.float32)).astype(np.float32)
-
-
-def _sample_pdf_ref(got_pdf, ref_pdf, ref_flag, pdf_at_gpu_dir):
-    """Reference for a sample's pdf, per lane: the reference's own sample pdf where the GPU value
-    already agrees with it (always on rejected lanes, flag None, whose all-zero direction has no
-    pdf) and otherwise the reference pdf evaluated at the GPU's direction (a sharp lobe amplifies
-    a 1-ulp direction difference beyond 1e-5).  Mixture samplers (AshikhminShirleyFull,
-    ashikhminshirleyfull.h:115-121) report the weighted pdfs of both candidate samples, which
-    is not pdf(direction); for them the first rule is the one that applies."""
-    raw = np.zeros(got_pdf.shape, bool)
-    raw[ou.parity_violations(got_pdf[None], ref_pdf[None])[1]] = True
-    raw = ~raw | (np.asarray(ref_flag) == 0)
-    return np.where(raw, ref_pdf, pdf_at_gpu_dir)
-
-
-def _stats(got, ref, floor):
-    sel = np.abs(ref) > floor
-    rel = ou.rel_err(got, ref)
-    return {"max_ulp": int(ou.ulp_diff(got, ref).max()),
-            "max_rel_above_floor": float(rel[sel].max()) if sel.any() else 0.0,
-            "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0))}
+def _save(tag, arr):
+    d = os.path.join(ou.ROOT, "gpurun_out", "gpu_outputs")
+    os.makedirs(d, exist_ok=True)
+    np.save(os.path.join(d, tag + ".npy"), arr)
 
 
 def _report(tag, stats):
-    import json
-    import os
     os.makedirs(os.path.join(ou.ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ou.ROOT, "gpurun_out", f"parity_{tag}.json"), "w") as f:
         json.dump(stats, f, indent=1)
@@ -108,11 +65,72 @@ def _report(tag, stats):
         print(f"{tag} {k}: {v}")
 
 
-def _save(tag, arr):
-    import os
-    d = os.path.join(ou.ROOT, "gpurun_out", "gpu_outputs")
-    os.makedirs(d, exist_ok=True)
-    np.save(os.path.join(d, tag + ".npy"), arr)
+def check_lanes(got, ref, what, provers=()):
+    """Apply the per-lane bar to (channels, lanes) arrays; lanes outside it must be proven by one of `provers`
+    (functions lanes -> bool array); returns the statistics reported under gpurun_out/parity_*.json."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    n = got.shape[-1]
+    ok = ou.parity_ok(got, ref).reshape(-1, n).all(0)
+    bad = np.nonzero(~ok)[0]
+    proven = {}
+    left = bad
+    for prove in provers:
+        if left.size == 0:
+            break
+        p = np.asarray(prove(left), bool)
+        proven[prove.__name__] = int(p.sum())
+        left = left[~p]
+    if left.size:
+        i = left[:4]
+        raise AssertionError(f"{what}: {left.size} of {n} lanes outside the 1e-5 bar and not proven; lanes {i}: "
+                             f"got {got[..., i].T.tolist()} ref {ref[..., i].T.tolist()}")
+    assert bad.size <= max(2, MAX_EXCUSED_FRAC * n), f"{what}: {bad.size} of {n} lanes needed a per-lane proof"
+    sub = (np.abs(ref) < ou.FLT_MIN) & (ref != 0)
+    return {"lanes": int(n), "max_rel_normal": ou.max_rel_normal(got, ref),
+            "max_ulp": int(ou.ulp_diff(got, ref).max()) if got.size else 0,
+            "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0)) if got.size else 1.0,
+            "subnormal_ref_values": int(sub.sum()), "lanes_outside_bar": int(bad.size),
+            "proven_by": proven}
+
+
+def _input_ulps_prover(ref_fn, inputs, got):
+    """Prover: the backward-error argument over the given lanes of `inputs` (list of (k, n) arrays)."""
+    def input_ulps(lanes):
+        return ou.explained_by_input_ulps(ref_fn, [a[:, lanes] for a in inputs], got[:, lanes])
+    return input_ulps
+
+
+def _sampler_prover(bbm, name, params, din, dout, pdf_got, eval_got=None, component=3, unit=0):
+    """Prover for the tabulated samplers' pdf: see the module docstring.  pdf_got: (n,) GPU pdfs of the pairs
+    (din, dout); eval_got: their (3, n) eval channels, which must meet the bar for a lane to be proven here."""
+    hb = ou.sampler_backscatter_dirs()
+    p = np.asarray(params, np.float32).copy()
+    if name == "NganHe":
+        p[:3] = 1.0          # scaledmodel wraps the sampler from outside: the CDF sees the unscaled he_base
+    m = bbm.BsdfModel(name)
+    m.set_parameter_values(p)
+    gpu_bs = _gpu_evalpdf(m, hb, hb, component=bbm.bsdf_flag(component), unit=bbm.unit_t(unit))
+    ref_bs = ou.oracle_eval_pdf(name, p, hb, hb, component, unit, nthreads=8)
+
+    def sampler_cdf(lanes):
+        if not ou.parity_ok(gpu_bs[:3], ref_bs[:3]).all():
+            return np.zeros(lanes.size, bool)
+        want = ou.sampler_pdf(ou.sampler_cdf(gpu_bs[:3]), din[:, lanes], dout[:, lanes])
+        ok = ou.parity_ok(pdf_got[lanes], want)
+        if eval_got is not None:
+            ok &= ou.parity_ok(eval_got[:, lanes], ou.oracle_eval_pdf(name, params, din[:, lanes], dout[:, lanes],
+                                                                      component, unit, nthreads=8)[:3]).all(0)
+        return ok
+    return sampler_cdf
+
+
+def _evalpdf_provers(bbm, name, params, din, dout, got, component=3, unit=0):
+    provers = [_input_ulps_prover(lambda a, b: ou.oracle_eval_pdf(name, params, a, b, component, unit, nthreads=8),
+                                  [din, dout], got)]
+    if name in TABULATED_SAMPLERS:
+        provers.append(_sampler_prover(bbm, name, params, din, dout, got[3], got[:3], component, unit))
+    return provers
 
 
 def _gpu_models(bbm):
@@ -120,35 +138,40 @@ def _gpu_models(bbm):
 
 
 def test_every_gpu_model_matches_reference_golden(bbm):
-    worst = {}
+    stats = {}
     for name in _gpu_models(bbm):
         g = ou.golden_model(name)
         for si in range(len(META["models"][name]["sets"])):
+            params = g[f"params{si}"]
             m = bbm.BsdfModel(name)
-            m.set_parameter_values(g[f"params{si}"])
+            m.set_parameter_values(params)
             got = _gpu_evalpdf(m, INP["pin"], INP["pout"])
             _save(f"golden_{name}_{si}", got)
-            worst[f"{name}[{si}]"] = _assert_parity(got, g[f"evalpdf{si}"], f"{name}[{si}]")
-    _report("golden", worst)
+            stats[f"{name}[{si}]"] = check_lanes(got, g[f"evalpdf{si}"], f"{name}[{si}]",
+                                                 _evalpdf_provers(bbm, name, params, INP["pin"], INP["pout"], got))
+    _report("golden", stats)
 
 
 def test_reflectance_matches_reference_golden(bbm):
     """reflectance(out) (concepts/bsdfmodel.h: Spectrum reflectance(out, component, unit, mask)) for
     every parameter set and per component; it is also the sampling weight of Aggregate models."""
-    worst = {}
+    stats = {}
     for name in _gpu_models(bbm):
         g = ou.golden_model(name)
         for si in range(len(META["models"][name]["sets"])):
+            params = g[f"params{si}"]
             m = bbm.BsdfModel(name)
-            m.set_parameter_values(g[f"params{si}"])
+            m.set_parameter_values(params)
             got = m.reflectance(_dev(INP["sout"])).cpu().numpy()
-            worst[f"{name}[{si}]"] = _assert_parity(got, g[f"reflectance{si}"], f"{name}[{si}] reflectance")
+            prove = _input_ulps_prover(lambda o, p=params: ou.ref_reflectance(name, p, o), [INP["sout"]], got)
+            stats[f"{name}[{si}]"] = check_lanes(got, g[f"reflectance{si}"], f"{name}[{si}] reflectance", [prove])
         m = bbm.BsdfModel(name)
         m.set_parameter_values(g["params0"])
         for tag, comp in (("diffuse", 1), ("specular", 2)):
             got = m.reflectance(_dev(INP["sout"]), component=bbm.bsdf_flag(comp)).cpu().numpy()
-            _assert_parity(got, g[f"reflectance_{tag}"], f"{name}/{tag} reflectance")
-    _report("reflectance", worst)
+            prove = _input_ulps_prover(lambda o, c=comp: ou.ref_reflectance(name, g["params0"], o, c), [INP["sout"]], got)
+            check_lanes(got, g[f"reflectance_{tag}"], f"{name}/{tag} reflectance", [prove])
+    _report("reflectance", stats)
 
 
 @pytest.mark.parametrize("tag,comp,unit", [("diffuse", 1, 0), ("specular", 2, 0), ("importance", 3, 1)])
@@ -158,7 +181,8 @@ def test_component_and_unit_semantics(bbm, tag, comp, unit):
         m = bbm.BsdfModel(name)
         m.set_parameter_values(g["params0"])
         got = _gpu_evalpdf(m, INP["pin"], INP["pout"], component=bbm.bsdf_flag(comp), unit=bbm.unit_t(unit))
-        _assert_parity(got, g[f"evalpdf_{tag}"], f"{name}/{tag}")
+        check_lanes(got, g[f"evalpdf_{tag}"], f"{name}/{tag}",
+                    _evalpdf_provers(bbm, name, g["params0"], INP["pin"], INP["pout"], got, comp, unit))
 
 
 def test_eval_pdf_fused_equals_separate_calls(bbm):
@@ -174,22 +198,27 @@ def test_eval_pdf_fused_equals_separate_calls(bbm):
         assert torch.equal(rgb, rgb2) and torch.equal(pdf, pdf2), name
 
 
-def test_large_batch_vs_oracle(bbm):
-    """1M pairs per model against the reference itself (prebuilt oracle/_ref shim) or, where it
-    is absent, the C restatement (bit-exact vs the reference on the golden vectors)."""
+@pytest.mark.parametrize("mode_in,mode_out", [(0, 1), (0, 0)])
+def test_large_batch_vs_reference(bbm, mode_in, mode_out):
+    """1M pairs per model and parameter set against the reference itself (prebuilt oracle/_ref shim): upper
+    hemisphere in with sphere out (~50 % masked lanes) and both on the upper hemisphere (every lane active)."""
     n = 1 << 20
-    din = bbm.fill_directions(0xBB5EED, 0, 0, n, mode=0)
-    dout = bbm.fill_directions(0xBB5EED, 1, 0, n, mode=1)
-    hin, hout = din.cpu().numpy(), dout.cpu().numpy()
+    din = bbm.fill_directions(0xBB5EED, 0, 0, n, mode=mode_in).cpu().numpy()
+    dout = bbm.fill_directions(0xBB5EED, 1, 0, n, mode=mode_out).cpu().numpy()
     stats = {}
     for name in _gpu_models(bbm):
         if name not in ou.oracle_models():
             continue
-        m = bbm.BsdfModel(name)
-        got = _gpu_evalpdf(m, hin, hout)
-        ref = ou.oracle_eval_pdf(name, m.parameter_values(), hin, hout, nthreads=8)
-        stats[name] = _assert_parity(got, ref, name)
-    _report("large", stats)
+        g = ou.golden_model(name)
+        for si in range(len(META["models"][name]["sets"])):
+            params = g[f"params{si}"]
+            m = bbm.BsdfModel(name)
+            m.set_parameter_values(params)
+            got = _gpu_evalpdf(m, din, dout)
+            ref = ou.oracle_eval_pdf(name, params, din, dout, nthreads=8)
+            stats[f"{name}[{si}]"] = check_lanes(got, ref, f"{name}[{si}] {mode_in}{mode_out}",
+                                                 _evalpdf_provers(bbm, name, params, din, dout, got))
+    _report(f"large_{mode_in}{mode_out}", stats)
 
 
 def test_mask_lanes_are_zero_and_others_untouched(bbm):
@@ -239,40 +268,120 @@ def test_errors_raise(bbm):
         m.eval_pdf(d, d[:, :8].contiguous())
     with pytest.raises(TypeError):
         m.eval_pdf(d.double(), d)
+    # caller-supplied outputs are validated before the launch (an undersized or foreign buffer would be written
+    # out of bounds by the kernel)
+    with pytest.raises(ValueError):
+        m.eval_pdf(d, d, rgb=torch.empty((3, 8), device="cuda"))
+    with pytest.raises(ValueError):
+        m.eval_pdf(d, d, pdf=torch.empty((15,), device="cuda"))
+    with pytest.raises(TypeError):
+        m.eval_pdf(d, d, rgb=torch.empty((3, 16), dtype=torch.float64, device="cuda"))
+    with pytest.raises(ValueError):
+        m.eval_pdf(d, d, rgb=torch.empty((16, 3), device="cuda").t())
 
 
-DIR_TOL_MAX = 1e-3
-
-# The He family samples its halfway vector from a 90-bin tabulated CDF (ndf/sampler.h:63-92, util/cdf.h:73-83)
-# whose within-bin warp is discontinuous at the bin edges (residual 1 of bin k maps to (k + 1.5) / 90, residual
-# 0 of bin k + 1 to (k + 0.5) / 90) and infinitely steep next to them.  The CDF entries are sums of backscatter
-# evaluations that agree with the reference to ~1e-5 relative, so an xi0 that close to an edge may land in the
-# neighbouring bin and move the direction by a bin width.  Such a lane passes when the reference itself, given
-# an xi0 at most FLIP_ULPS float steps away, returns the GPU's direction (to FLIP_DIR_TOL: the warp is steep
-# there); at most FLIP_MAX_FRAC of the lanes may need this.
-TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
+# ----------------------------------------------------------------------------------------------- sampling
+#
+# Directions are unit vectors: a sample's direction meets the bar where every component is within 1e-5 of the
+# reference's (1e-5 of the vector's length).  A lane outside it must be proven, like an eval lane, by the
+# reference at inputs (out, xi) moved by <= 2 float steps; for the tabulated samplers also by a CDF bin flip:
+# the sampled bin's within-bin warp is discontinuous at the bin edges (ndf/sampler.h:63-92, util/cdf.h:73-83)
+# and a 1-ulp CDF difference moves an xi0 that close to an edge into the neighbouring bin, so such a lane
+# passes when the reference, given an xi0 at most FLIP_ULPS float steps away, returns the GPU's direction
+# (to FLIP_DIR_TOL: the warp is steep there).  Flags must be identical, and the pdf of a sample is checked
+# with the eval bar against the reference's pdf at the GPU's own direction.
+DIR_TOL = 1e-5
 FLIP_ULPS = 1024
 FLIP_DIR_TOL = 1e-4
-FLIP_MAX_FRAC = 1e-3
 
 
-def _far_lanes_explained_by_bin_flips(name, params, dout, xi, got_dir, derr, component=3):
-    """Indices of lanes with a direction error > DIR_TOL_MAX that no nearby xi0 explains."""
-    far = np.nonzero(derr.max(0) > DIR_TOL_MAX)[0]
-    if name not in TABULATED_SAMPLERS or far.size == 0:
-        return far
-    assert far.size <= max(1, FLIP_MAX_FRAC * derr.shape[1]), f"{name}: {far.size} bin-edge lanes"
-    x0 = xi[0, far].astype(np.float32)
-    steps = np.concatenate([-np.arange(1, FLIP_ULPS + 1), np.arange(1, FLIP_ULPS + 1)])
-    # x0 moved by k float steps (k * ulp(x0): exact for the xi0 of [0, 1) away from powers of two)
-    ulp = np.spacing(x0)
-    xs = np.clip(x0[:, None] + steps[None, :].astype(np.float32) * ulp[:, None], 0, 1).astype(np.float32)
-    m = steps.size
-    o = np.ascontiguousarray(np.repeat(dout[:, far], m, axis=1))
-    x = np.ascontiguousarray(np.stack([xs.ravel(), np.repeat(xi[1, far], m)]).astype(np.float32))
-    ref, _ = ou.oracle_sample(name, params, o, x, component=component, nthreads=8)
-    d = np.abs(np.repeat(got_dir[:, far], m, axis=1) - ref[:3]).max(0).reshape(far.size, m)
-    return far[np.nanmin(d, axis=1) > FLIP_DIR_TOL]
+def _dir_ok(got, ref):
+    with np.errstate(invalid="ignore"):
+        return ((np.abs(np.asarray(got, np.float64) - ref) <= DIR_TOL) |
+                (np.isnan(got) & np.isnan(ref))).all(0)
+
+
+def _sample_dir_provers(name, params, dout, xi, got_dir, component=3):
+    def input_ulps(lanes):
+        def ref_dirs(o, x):
+            d, _ = ou.oracle_sample(name, params, o, x, component=component, nthreads=8)
+            return d[:3]
+        r = ou.explained_by_input_ulps(ref_dirs, [dout[:, lanes], xi[:, lanes]], got_dir[:, lanes])
+        # for directions the 1e-5 bar is absolute; explained_by_input_ulps's bracket test covers that too
+        return r
+
+    def cdf_bin_flip(lanes):
+        if name not in TABULATED_SAMPLERS:
+            return np.zeros(lanes.size, bool)
+        x0 = xi[0, lanes].astype(np.float32)
+        steps = np.concatenate([-np.arange(1, FLIP_ULPS + 1), np.arange(1, FLIP_ULPS + 1)])
+        xs = ou.perturb_ulps(np.repeat(x0[:, None], steps.size, 1), np.broadcast_to(steps, (x0.size, steps.size)))
+        xs = np.clip(xs, 0, 1).astype(np.float32)
+        m = steps.size
+        o = np.ascontiguousarray(np.repeat(dout[:, lanes], m, axis=1))
+        x = np.ascontiguousarray(np.stack([xs.ravel(), np.repeat(xi[1, lanes], m)]).astype(np.float32))
+        ref, _ = ou.oracle_sample(name, params, o, x, component=component, nthreads=8)
+        d = np.abs(np.repeat(got_dir[:, lanes], m, axis=1) - ref[:3]).max(0).reshape(lanes.size, m)
+        return np.nanmin(d, axis=1) <= FLIP_DIR_TOL
+    return [input_ulps, cdf_bin_flip]
+
+
+def _pdf_at_dir(name, params, dirs, outs, xi, flags):
+    """The pdf the reference's sampler would report for a sample at `dirs`.  For every model but
+    one that is pdf(dir, out).  AshikhminShirleyFull's one-sample mixture
+    (ashikhminshirleyfull.h:96-124) draws a specular candidate with xi0 / w_s and a diffuse one
+    with (xi0 - w_s) / w_d (0 when w_d <= eps), returns the one selected by xi0 <= w_s, and
+    reports w_s pdf_s(specular candidate) + w_d pdf_d(diffuse candidate): the chosen candidate's
+    pdf is taken at the GPU direction, the other candidate is drawn by the reference itself."""
+    if name != "AshikhminShirleyFull":
+        return ou.oracle_eval_pdf(name, params, dirs, outs, nthreads=8)[3]
+    p = np.asarray(params, np.float32)
+    one, eps = np.float32(1), np.finfo(np.float32).eps
+    spec_albedo = (p[3] + p[4]) + p[5]
+    diff_albedo = ((p[0] + p[1]) + p[2]) * (one - spec_albedo)
+    dw = diff_albedo / (diff_albedo + spec_albedo)
+    sw = one - dw
+    xi = np.asarray(xi, np.float32)
+    xs = np.stack([xi[0] / sw if sw > eps else np.zeros_like(xi[0]), xi[1]])
+    xd = np.stack([(xi[0] - sw) / dw if dw > eps else np.zeros_like(xi[0]), xi[1]])
+    flags = np.asarray(flags)
+    ps = np.where(flags == 2, ou.oracle_eval_pdf(name, params, dirs, outs, component=2, nthreads=8)[3],
+                  ou.oracle_sample(name, params, outs, xs, component=2, nthreads=8)[0][3])
+    pd = np.where(flags == 1, ou.oracle_eval_pdf(name, params, dirs, outs, component=1, nthreads=8)[3],
+                  ou.oracle_sample(name, params, outs, xd, component=1, nthreads=8)[0][3])
+    return (sw * ps.astype(np.float32) + dw * pd.astype(np.float32)).astype(np.float32)
+
+
+def _check_samples(bbm, name, params, sout, sxi, got, flag, ref, ref_flag, what):
+    """Flags identical; directions per lane (bar or proof); sample pdf vs the reference pdf at the GPU's
+    direction (the reference's own sample pdf on rejected lanes, whose all-zero direction has no pdf)."""
+    assert np.array_equal(np.asarray(flag).astype(np.uint32), np.asarray(ref_flag).astype(np.uint32)), f"{what} flags"
+    dok = _dir_ok(got[:3], ref[:3])
+    bad = np.nonzero(~dok)[0]
+    proven = {}
+    left = bad
+    for prove in _sample_dir_provers(name, params, sout, sxi, got[:3]):
+        if left.size == 0:
+            break
+        p = prove(left)
+        proven[prove.__name__] = int(p.sum())
+        left = left[~p]
+    assert left.size == 0, (f"{what}: {left.size} sample directions outside 1e-5 and not proven, lanes {left[:4]}: "
+                            f"got {got[:3, left[:4]].T.tolist()} ref {ref[:3, left[:4]].T.tolist()}")
+    assert bad.size <= max(2, MAX_EXCUSED_FRAC * dok.size), f"{what}: {bad.size} directions needed a proof"
+    rejected = np.asarray(ref_flag) == 0
+    pref = np.where(rejected, ref[3], _pdf_at_dir(name, params, got[:3], sout, sxi, flag))
+    provers = [] if name == "AshikhminShirleyFull" else \
+        [_input_ulps_prover(lambda a, b: ou.oracle_eval_pdf(name, params, a, b, nthreads=8)[3:], [got[:3], sout],
+                            got[3:])]
+    if name in TABULATED_SAMPLERS:
+        provers.append(_sampler_prover(bbm, name, params, got[:3], sout, got[3]))
+    st = check_lanes(got[3:], pref[None], f"{what} pdf(dir)", provers)
+    st["max_dir_abs_err"] = float(np.nanmax(np.abs(got[:3].astype(np.float64) - ref[:3]))) if got.size else 0.0
+    st["frac_dir_within_1e-6"] = float(np.mean(np.abs(got[:3].astype(np.float64) - ref[:3]).max(0) <= 1e-6))
+    st["dir_lanes_outside_bar"] = int(bad.size)
+    st["dir_proven_by"] = proven
+    return st
 
 
 def _gpu_sample(model, sout, sxi, **kw):
@@ -282,73 +391,43 @@ def _gpu_sample(model, sout, sxi, **kw):
 
 
 def test_sample_matches_reference_golden(bbm):
-    """sample(out, xi) -> (direction, pdf, flag) vs the reference's own samples.
-
-    Directions are unit vectors compared per component.  Beckmann VNDF sampling inverts the slope
-    CDF with three Newton steps on erfinv (ndf/beckmann.h:92-110); at clamped xi (0.9999999) and a
-    grazing view it is ill-conditioned: swapping glibc's erff for a 1-ulp-different erf in the C
-    restatement alone moves the direction by 1.09e-5 (tests/golden CookTorrance set 2, sample 666).
-    The same edge cases with a rougher lobe reach ~5e-5.  The bar is therefore: |d_gpu - d_ref| <=
-    1e-5 on >= 99.5% of samples and <= 1e-3 everywhere (a wrong formula moves directions by O(0.1)),
-    flags identical, and the pdf of every GPU sample equal (1e-5) to the reference pdf evaluated at
-    that GPU direction."""
+    """sample(out, xi) -> (direction, pdf, flag) vs the reference's own samples (golden)."""
     stats = {}
     for name in _gpu_models(bbm):
         g = ou.golden_model(name)
         for si in range(len(META["models"][name]["sets"])):
+            params = g[f"params{si}"]
             m = bbm.BsdfModel(name)
-            m.set_parameter_values(g[f"params{si}"])
+            m.set_parameter_values(params)
             got, flag = _gpu_sample(m, INP["sout"], INP["sxi"])
             _save(f"sample_{name}_{si}", np.concatenate([got, flag[None].astype(np.float32)], 0))
-            ref = g[f"sample{si}"]
-            assert np.array_equal(flag.astype(np.uint8), g[f"sflag{si}"]), f"{name}[{si}] flags"
-            derr = np.abs(got[:3].astype(np.float64) - ref[:3])
-            far = _far_lanes_explained_by_bin_flips(name, g[f"params{si}"], INP["sout"], INP["sxi"], got[:3], derr)
-            assert far.size == 0, f"{name}[{si}] direction err {np.nanmax(derr):.3e}"
-            assert np.mean(derr.max(0) > 1e-5) <= 0.005, f"{name}[{si}] too many directions off by > 1e-5"
-            # the pdf of a sample is pdf(direction): for a sharp lobe a 1-ulp direction difference
-            # moves it by more than 1e-5, so it is checked at the GPU's own direction (reference
-            # pdf via the bit-exact restatement) and the raw difference is reported
-            # lanes the reference rejects (flag None: invalid xi / component / below the surface)
-            # return the all-zero sample; pdf(0-vector) is undefined there, so they compare to 0
-            pref = _sample_pdf_ref(got[3], ref[3], g[f"sflag{si}"],
-                                   _pdf_at_dir(name, g[f"params{si}"], got[:3], INP["sout"], INP["sxi"], flag))
-            st = _assert_parity(got[3:], pref[None], f"{name}[{si}] pdf(dir)")
-            st["max_dir_abs_err"] = float(np.nanmax(derr))
-            st["frac_dir_within_1e-6"] = float(np.mean(derr.max(0) <= 1e-6))
-            st["frac_dir_within_1e-5"] = float(np.mean(derr.max(0) <= 1e-5))
-            st["raw_pdf_max_rel"] = float(ou.rel_err(got[3], ref[3]).max())
-            stats[f"{name}[{si}]"] = st
+            stats[f"{name}[{si}]"] = _check_samples(bbm, name, params, INP["sout"], INP["sxi"], got, flag,
+                                                    g[f"sample{si}"], g[f"sflag{si}"], f"{name}[{si}]")
     _report("sample", stats)
 
 
-def test_sample_large_batch_vs_oracle(bbm):
+def test_sample_large_batch_vs_reference(bbm):
     n = 1 << 20
     out = bbm.fill_directions(0xBB5EED, 2, 0, n, mode=1)
     xi = torch.rand((2, n), generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")
     hout, hxi = out.cpu().numpy(), xi.cpu().numpy()
+    stats = {}
     for name in _gpu_models(bbm):
         if name not in ou.oracle_models():
             continue
         m = bbm.BsdfModel(name)
+        params = m.parameter_values()
         s = m.sample(out, xi)
         torch.cuda.synchronize()
         got = np.concatenate([s.direction.cpu().numpy(), s.pdf.cpu().numpy()[None]], 0)
-        ref, flag = ou.oracle_sample(name, m.parameter_values(), hout, hxi, nthreads=8)
-        assert np.array_equal(s.flag.cpu().numpy().astype(np.uint32), flag), name
-        derr = np.abs(got[:3].astype(np.float64) - ref[:3])
-        far = _far_lanes_explained_by_bin_flips(name, m.parameter_values(), hout, hxi, got[:3], derr)
-        assert far.size == 0, f"{name}: {far.size} directions off by > {DIR_TOL_MAX}, e.g. lane {far[:3]}"
-        assert np.mean(derr.max(0) > 1e-5) <= 0.005, name
-        pref = _sample_pdf_ref(got[3], ref[3], flag,
-                               _pdf_at_dir(name, m.parameter_values(), got[:3], hout, hxi, s.flag.cpu().numpy()))
-        _assert_parity(got[3:], pref[None], f"{name} pdf(dir)")
+        ref, flag = ou.oracle_sample(name, params, hout, hxi, nthreads=8)
+        stats[name] = _check_samples(bbm, name, params, hout, hxi, got, s.flag.cpu().numpy(), ref, flag, name)
+    _report("sample_large", stats)
 
 
 def test_cpp_adapter_drop_in(bbm):
     """backbone/hip C++ adapter: the same bbm::bsdfmodel<> instances (reference template API) on the
     CPU (native backbone) and through bbm::hip::{eval_pdf, sample} on the GPU (tests/cpp)."""
-    import os
     import subprocess
     exe = os.path.join(ou.ROOT, "tests", "cpp", "_build", "adapter_check")
     if not os.path.exists(exe):
@@ -386,7 +465,7 @@ def test_epd_g1_table_matches_reference(bbm):
     # 96 % of the entries are identical.  The rest differ by a few units in the 6th digit (<= 1.0e-5
     # relative): the shipped G1.h was generated by a build whose flags are not recorded (e.g. FMA
     # contraction of `integral += dq * exp(...)`, which the recurrence's cancellation amplifies), while this
-    # restatement evaluates every float op on its own.  The EPD outputs built on the table stay within
-    # ~2e-6 of the reference's (test_every_gpu_model_matches_reference_golden, test_large_batch_vs_oracle).
+    # restatement evaluates every float op on its own.  The EPD outputs built on the table meet the per-lane
+    # bar (test_every_gpu_model_matches_reference_golden, test_large_batch_vs_reference).
     assert exact > 0.95 and np.mean(diff <= 1.001 * digit) > 0.95
     assert rel.max() <= 2e-5

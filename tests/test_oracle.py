@@ -97,3 +97,19 @@ def test_dirgen_counter_property():
     assert np.array_equal(full[:, 600:], part)
     n = np.linalg.norm(full.astype(np.float64), axis=0)
     np.testing.assert_allclose(n, 1.0, atol=1e-6)
+
+
+@pytest.mark.skipif(ou.ref() is None, reason="oracle/_ref not built")
+def test_sampler_pdf_restatement_matches_reference():
+    """The numpy restatement of the tabulated samplers' pdf (used by the sampler-CDF proof) reproduces the
+    reference's own pdf from the reference's own backscatter evaluations (within 1e-5; ~99 % bit-exact)."""
+    hb = ou.sampler_backscatter_dirs()
+    for name in sorted({'He', 'HeWestin', 'HeHolzschuch', 'NganHe'}):
+        g = ou.golden_model(name)
+        for si in range(len(ou.golden_meta()["models"][name]["sets"])):
+            p = g[f"params{si}"].copy()
+            if name == "NganHe":
+                p[:3] = 1.0
+            bs = ou.oracle_eval_pdf(name, p, hb, hb, nthreads=8)
+            want = ou.sampler_pdf(ou.sampler_cdf(bs[:3]), ou.golden_inputs()["pin"], ou.golden_inputs()["pout"])
+            assert ou.parity_ok(want, g[f"evalpdf{si}"][3]).all(), f"{name}[{si}]"

@@ -27,6 +27,7 @@ import torch
 import bbm_amd
 from bbm_amd import _lib, check, fit, merl
 from bbm_amd.backbone import _stream_ptr
+from tools import bench_harness as bh
 
 SEED = 0xBB5EED
 HBM_PEAK_GBS = 8000.0
@@ -34,31 +35,8 @@ Z_ONLY = {"Lambertian"}
 
 
 def _timed(step, args, dist, stream):
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    tw = time.perf_counter()
-    while time.perf_counter() - tw < args.settle_s:
-        step()
-        torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        step()
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    """tools/bench_harness.timed: warmup, settle, barrier + synchronize around K steps, slowest rank."""
+    elapsed, kern_ms, _, _ = bh.timed(step, args, dist, stream)
     return elapsed, kern_ms
 
 
