@@ -215,30 +215,6 @@ struct He
     return (sigma0 > kEpsF) ? r : 0.0f;
   }
 
-  // The reference's Taylor terms m - 1 and m (he.h:452-455) rounded as it rounds them: gm chain in float with
-  // double factors g / m, eb / m in float, term in double with a double exp.  Term 0 is the loop's initial 0.
-  struct TermPair { float t[3], l[3]; };
-  __device__ __attribute__((noinline)) static TermPair exact_terms(double g0, double g1, double g2, float eb0, float eb1,
-                                                                   float eb2, int m)
-  {
-    TermPair r;
-    const double g[3] = {g0, g1, g2};
-    const float eb[3] = {eb0, eb1, eb2};
-    for (int c = 0; c < 3; ++c)
-    {
-      float gmc = 1.0f, t = 0.0f, l = 0.0f;
-      for (int k = 1; k <= m; ++k)
-      {
-        l = t;
-        gmc = float(double(gmc) * (g[c] / double(k)));
-        t = float(exp(-g[c] - double(eb[c] / float(k))) * double(gmc) / double(k));
-      }
-      r.t[c] = t;
-      r.l[c] = l;
-    }
-    return r;
-  }
-
   // D (he.h:411-467), Eqs. 78-79: Taylor series in g with Beckmann's rough approximation blended in
   __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
   {
@@ -271,59 +247,40 @@ struct He
     }
     float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
     bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
-    // term = exp(-g - eb/m) gm / m in double by the reference, gm = float(gm * (g / m)) a float rounded per step
-    // (Spectrum *= array<double>), eb/m a float quotient.  gm and eb/m are formed exactly that way here; the
-    // exponential is split as exp(-g) (once per channel) x exp(-eb/m) (accurate float exp per term), so a term
-    // is within ~4 ulp of the reference's and the loop body has no double exp.  The series only runs for
-    // min(g) <= APPROX + 1, so g <= (APPROX + 1) (0.645 / 0.444)^2 < 45: exp(-g) stays a normal float.
+    // term = float(exp(-g - eb/m) gm / m) in double (he.h:454), gm = float(gm * (g / m)) rounded per step
+    // (Spectrum *= array<double>), eb/m a float quotient -- formed here exactly that way, with the one double
+    // exponential split into exp(-g) (once per channel) x exp(-eb/m) (per term; exp_dd, a short f64 polynomial
+    // instead of the library's 42-instruction exp): the product agrees with the reference's exponential to
+    // ~2^-44, so every float term -- subnormal ones included -- is the reference's own rounding of it except
+    // within ~2^-20 ulp of a rounding midpoint.  That matters beyond accuracy: the adaptive stop (he.h:460)
+    // compares consecutive terms, and near the series' peak they are nearly equal, so terms that differed by
+    // an ulp would truncate the series one term early or late where D is tiny.
     double eg[3];
-    float egf[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-    {
-      if (APPROX >= 0) egf[c] = converged ? 0.0f : exp_d2f(-g[c]) * 1.15292150e+18f;   // x 2^60 (exact)
-      else eg[c] = exp(-g[c]);
-    }
+    for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp_dd(-g[c]);
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);
-      const float mf = float(m);
-      // exp(-eb/m) 2^60 (normal down to eb/m = 131: below that the term is < 2^-190 and rounds to 0 anyway) and
-      // exp(-g) 2^60: the products stay normal floats and one final scaling by 2^-120 rounds a term that is
-      // subnormal in the reference's double arithmetic once, as the reference's float(term) does
-      float ex[3];
+      const float mf = float(m), rmf = float(rm);
+      double ex[3];
       if (WESTIN)
       {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) ex[c] = expf_scaled60(-div_small(eb[c], mf, float(rm)));
+        for (int c = 0; c < 3; ++c) ex[c] = exp_dd(-double(div_small(eb[c], mf, rmf)));
       }
-      else ex[0] = ex[1] = ex[2] = expf_scaled60(-div_small(eb[0], mf, float(rm)));
+      else ex[0] = ex[1] = ex[2] = exp_dd(-double(div_small(eb[0], mf, rmf)));   // eb is the same for every channel
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
         last[c] = term[c];
         gm[c] = float(double(gm[c]) * (g[c] * rm));
-        if (APPROX >= 0) term[c] = ((egf[c] * gm[c]) * (ex[c] * float(rm))) * 7.52316385e-37f;   // 2^-120
-        else term[c] = float(eg[c] * double(ex[c]) * double(gm[c]) * rm * 8.6736173798840355e-19);   // eg unscaled: 2^-60
+        term[c] = float(eg[c] * ex[c] * double(gm[c]) * rm);
         sum[c] += term[c];
       }
+      // converged |= hmin(term) < eps && hmin(term) < hmin(last) (he.h:460)
       if (ADAPTIVE)
-      {
-        // converged |= hmin(term) < eps && hmin(term) < hmin(last) (he.h:460).  Near the series' peak the
-        // terms are nearly equal and a few-ulp difference would flip the test, truncating the sum one term
-        // early or late (a large relative change where D is tiny): where either comparison is within 1e-6,
-        // the decision is taken on the reference's exactly rounded terms m - 1 and m instead (terms below 2^-100 are
-        // rounded once from exact products already, see above).
-        float tmin = fminf(fminf(term[0], term[1]), term[2]);
-        float lmin = fminf(fminf(last[0], last[1]), last[2]);
-        if ((lmin >= 7.88860905e-31f && __builtin_fabsf(tmin - lmin) <= 1e-6f * lmin) || __builtin_fabsf(tmin - kEpsF) <= 1e-6f * kEpsF)
-        {
-          const TermPair x = exact_terms(g[0], g[1], g[2], eb[0], WESTIN ? eb[1] : eb[0], WESTIN ? eb[2] : eb[0], m);
-          tmin = fminf(fminf(x.t[0], x.t[1]), x.t[2]);
-          lmin = fminf(fminf(x.l[0], x.l[1]), x.l[2]);
-        }
-        converged = (tmin < kEpsF) && (tmin < lmin);
-      }
+        converged = (fminf(fminf(term[0], term[1]), term[2]) < kEpsF) &&
+                    (fminf(fminf(term[0], term[1]), term[2]) < fminf(fminf(last[0], last[1]), last[2]));
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], rough[c], weight)));

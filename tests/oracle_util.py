@@ -211,14 +211,17 @@ def perturb_ulps(a, steps):
     return out
 
 
-def explained_by_input_ulps(ref_fn, inputs, got, k=2, trials=48, seed=1234):
+def explained_by_input_ulps(ref_fn, inputs, got, k=2, trials=48, seed=1234, any_match=False, abs_tol=0.0):
     """Per-lane proof for lanes outside the bar (backward error): True for a lane where every output channel of
     the GPU lies within the bar of -- or between -- the reference's own outputs at inputs whose coordinates are
     each moved by at most k float steps (the unmoved input and `trials - 1` random moves, seeded).  Such a lane's
     difference is the reference's own sensitivity to the last bits of its input (subnormal intermediates,
     cancellation), not a different computation.
       ref_fn(*inputs) -> (c, n) reference outputs; inputs: list of (k_i, n) float32 arrays (directions, xi);
-      got: (c, n) GPU outputs of the lanes to prove."""
+      got: (c, n) GPU outputs of the lanes to prove.
+    any_match: also accept a lane where one moved input reproduces every channel within the bar (the test for
+    vector-valued outputs such as sampled directions, whose components move together).
+    abs_tol: an absolute floor for the bar (unit vectors: 1e-5 of the vector's length)."""
     inputs = [np.asarray(a, np.float32) for a in inputs]
     got = np.asarray(got, np.float64)
     n = got.shape[1]
@@ -234,9 +237,57 @@ def explained_by_input_ulps(ref_fn, inputs, got, k=2, trials=48, seed=1234):
     with np.errstate(invalid="ignore"):
         lo = np.nanmin(r, axis=1)
         hi = np.nanmax(r, axis=1)
-        tol = REL_TOL * np.maximum(np.maximum(np.abs(lo), np.abs(hi)), FLT_MIN)
-        ok = ((got >= lo - tol) & (got <= hi + tol)) | (np.isnan(got) & np.isnan(r).any(axis=1))
-    return ok.all(axis=0)
+        tol = np.maximum(REL_TOL * np.maximum(np.maximum(np.abs(lo), np.abs(hi)), FLT_MIN), abs_tol)
+        ok = (((got >= lo - tol) & (got <= hi + tol)) | (np.isnan(got) & np.isnan(r).any(axis=1))).all(axis=0)
+        if any_match:
+            near = np.abs(r - got[:, None, :]) <= np.maximum(REL_TOL * np.maximum(np.abs(r), FLT_MIN), abs_tol)
+            ok |= near.all(axis=0).any(axis=0)
+    return ok
+
+
+LIBM_FNS = ["erff", "erfcf", "expf", "logf", "powf", "sinf", "cosf", "tanf", "atanf", "atan2f", "acosf",
+            "sincosf(sin)", "sincosf(cos)", "tgammaf"]     # oracle/libm_ulp.c's order
+
+
+def explained_by_libm_ulp(ref_fn, inputs, got, max_calls=8, any_match=False, abs_tol=0.0):
+    """Per-lane proof (libm last bit): True for a lane where the reference itself reproduces the GPU value (every
+    channel within the bar) when ONE call of one glibc float function returns its neighbouring float (or all
+    calls of it do) -- oracle/libm_ulp.c.  glibc's erff/erfcf are not correctly rounded on ~6 % of inputs, so an
+    ill-conditioned output (an inverse-CDF sample at a clamped xi) can hinge on that last bit alone.
+      ref_fn(*inputs) -> (c, n): the reference, called here with one lane at a time in this thread (nthreads=1:
+      the perturbation switch is per thread)."""
+    lib = ref()
+    got = np.asarray(got, np.float64)
+    n = got.shape[1]
+    proven = np.zeros(n, bool)
+    if lib is None or n == 0:
+        return proven
+    nfn = lib.bbmref_libm_nfn()
+
+    def match(r, g):
+        with np.errstate(invalid="ignore"):
+            tol = np.maximum(REL_TOL * np.maximum(np.abs(r), FLT_MIN), abs_tol)
+            return bool(((np.abs(r - g) <= tol) | (r == g) | (np.isnan(r) & np.isnan(g))).all())
+    try:
+        for i in range(n):
+            ins = [np.ascontiguousarray(np.asarray(a, np.float32)[:, i:i + 1]) for a in inputs]
+            lib.bbmref_libm_ulp(-1, -1, 0)
+            ref_fn(*ins)
+            counts = [lib.bbmref_libm_calls(f) for f in range(nfn)]
+            for f in range(nfn):
+                if proven[i] or counts[f] <= 0:
+                    continue
+                for call in list(range(min(counts[f], max_calls))) + [-1]:
+                    for u in (-1, 1):
+                        lib.bbmref_libm_ulp(f, call, u)
+                        if match(np.asarray(ref_fn(*ins), np.float64)[:, 0], got[:, i]):
+                            proven[i] = True
+                            break
+                    if proven[i]:
+                        break
+    finally:
+        lib.bbmref_libm_ulp(-1, -1, 0)
+    return proven
 
 
 # ----------------------------------------------------------------- data-driven sampler pdf (He family, Merl)
