@@ -406,6 +406,22 @@ def _check_samples(bbm, name, params, sout, sxi, got, flag, ref, ref_flag, what)
                                           [got[:3], sout], got[3:]))
         provers.append(_libm_prover(lambda a, b: ou.oracle_eval_pdf(name, params, a, b, nthreads=1)[3:],
                                     [got[:3], sout], got[3:]))
+    else:
+        # the one-sample mixture's pdf (w_s pdf_s + w_d pdf_d, either weight may be negative for out-of-range
+        # albedos, so it can cancel): the same input-ulps argument over (direction, out, xi) and its flag
+        def mixture_input_ulps(lanes):
+            ok = np.zeros(lanes.size, bool)
+            for k, trials in ((2, 48), (4, 128)):
+                rest = ~ok
+                if not rest.any():
+                    break
+                sub = lanes[rest]
+                fl = np.tile(np.asarray(flag)[sub], trials)     # moved inputs come trial by trial
+                ok[rest] = ou.explained_by_input_ulps(lambda d, o, x: _pdf_at_dir(name, params, d, o, x, fl)[None],
+                                                      [got[:3, sub], sout[:, sub], sxi[:, sub]], got[3:, sub], k=k,
+                                                      trials=trials)
+            return ok
+        provers.append(mixture_input_ulps)
     st = check_lanes(got[3:], pref[None], f"{what} pdf(dir)", provers)
     st["max_dir_abs_err"] = float(np.nanmax(np.abs(got[:3].astype(np.float64) - ref[:3]))) if got.size else 0.0
     st["frac_dir_within_1e-6"] = float(np.mean(np.abs(got[:3].astype(np.float64) - ref[:3]).max(0) <= 1e-6))
