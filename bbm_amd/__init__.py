@@ -9,13 +9,13 @@ name, `fromString` / `bsdf_import`, `bsdf_flag`, `unit_t`, `BsdfSample`, and bat
 Importing the package loads the HIP library; if it is missing the import fails loudly.
 """
 from . import _lib
-from .backbone import (Aggregate, BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString,
+from .backbone import (Aggregate, AggregateModel, BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString,
                        model_names, unit_t, _make_ctor)
 from .models import ATTRIBUTES
 
 _lib.load()
 
-__all__ = ["Aggregate", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
+__all__ = ["Aggregate", "AggregateModel", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
            "fill_directions", "ATTRIBUTES"]
 
 from .merl import Merl  # noqa: E402  -- measured data: constructed from a file, not from attributes

@@ -54,7 +54,15 @@ SIGNATURES = {
     "bbm_hip_check_draws": (_I, [_I, _U64, _I, _I, _U64, _SZ, _P, _P, _P]),
     "bbm_hip_check_trials": (_I, [_I, _U64, _I, _I, _P, _P, _P, _P]),
     "bbm_hip_sphere_dirs": (_I, [_P, _P, _SZ, _I, _P, _P, _P, _P]),
+    "bbm_hip_aggregate_eval_pdf": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
+    "bbm_hip_aggregate_sample": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "bbm_hip_aggregate_reflectance": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
 }
+
+
+class Child(ctypes.Structure):
+    """bbm_hip_child (include/bbm_hip.h): one child of a composed aggregate."""
+    _fields_ = [("model_id", ctypes.c_int), ("params", ctypes.c_void_p), ("nparams", ctypes.c_int)]
 
 
 class BackboneError(RuntimeError):

@@ -181,7 +181,12 @@ class BsdfModel:
     def set_attribute(self, attr, value):
         k, shape = self._slot(attr)
         n = attr_size(shape)
-        v = np.asarray(value, dtype=np.float32).reshape(-1)
+        src = np.asarray(value, dtype=np.float64).reshape(-1)
+        with np.errstate(over="ignore"):
+            v = src.astype(np.float32)
+        if np.any(np.isfinite(src) & ~np.isfinite(v)):
+            # the reference's string conversion refuses a value beyond the float range (std::out_of_range)
+            raise ValueError(f"{self.name}.{attr}: value out of the float range: {src[np.isfinite(src) & ~np.isfinite(v)]}")
         if v.size == 1 and n > 1:      # a scalar broadcasts over an RGB / Vec2d attribute
             v = np.repeat(v, n)
         if v.size != n:
@@ -370,10 +375,7 @@ def _parse_model(tok, i, s):
             kids.append(m)
             if tok[i] == ",":
                 i += 1
-        key = aggregate_key([k.name for k in kids])
-        if key not in AGGREGATES:
-            raise ValueError(f"unsupported aggregate: {key}")
-        return BsdfModel(key, *kids), i + 1
+        return Aggregate(*kids), i + 1
     if name not in ATTRIBUTES:
         raise ValueError(f"unknown BSDF model: {name}")
     m = BsdfModel(name)
@@ -388,7 +390,7 @@ def _parse_model(tok, i, s):
             attr = layout[pos_idx]
             v, i = _parse_value(tok, i)
         pos_idx += 1
-        m.set_attribute(attr, np.asarray(v, dtype=np.float32))
+        m.set_attribute(attr, np.asarray(v, dtype=np.float64))
         if tok[i] == ",":
             i += 1
     return m, i + 1
@@ -413,12 +415,122 @@ def fromString(s):
 bsdf_import = fromString
 
 
-def Aggregate(*children):
-    """aggregate(models...) (aggregatemodel.h:232-233) for the supported Aggregate(Lambertian, X) forms."""
+class AggregateModel:
+    """aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 models that have kernels
+    of their own (single models or fused aggregates), evaluated by composing the children's kernels
+    (bbm_hip_aggregate_*, bbm_amd/csrc/composite.hip): eval / reflectance = the children's sum (right fold),
+    pdf = their reflectance-weighted mixture, sample = the reference's child selection on xi0.  The published
+    fits' form Aggregate(Lambertian, X) has fused kernels instead (Aggregate(...) picks them).  Parameters are
+    the children's vectors in order (reflection order of the base classes)."""
+
+    def __init__(self, *children):
+        if len(children) < 2:
+            raise ValueError("an aggregate needs at least two child models")
+        for c in children:
+            if not isinstance(c, BsdfModel):
+                raise TypeError("aggregate children must be BsdfModel instances with kernels of their own "
+                                "(nested composed aggregates are not supported)")
+        self._children = [BsdfModel(c.name) for c in children]
+        for mine, c in zip(self._children, children):
+            mine._params[:] = c._params
+        self.name = aggregate_key([c.name for c in children])
+
+    def children(self):
+        out = []
+        for c in self._children:
+            m = BsdfModel(c.name)
+            m._params[:] = c._params
+            out.append(m)
+        return out
+
+    def parameter_values(self, flag=None):
+        return np.concatenate([c.parameter_values(flag) for c in self._children])
+
+    def set_parameter_values(self, values):
+        v = np.asarray(values, dtype=np.float32).reshape(-1)
+        if v.size != sum(c._params.size for c in self._children):
+            raise ValueError(f"{self.name}: expected {sum(c._params.size for c in self._children)} parameters")
+        k = 0
+        for c in self._children:
+            c._params[:] = v[k:k + c._params.size]
+            k += c._params.size
+
+    def __str__(self):
+        return "Aggregate(" + ", ".join(str(c) for c in self._children) + ")"
+
+    __repr__ = __str__
+
+    def _desc(self):
+        arr = (_lib.Child * len(self._children))()
+        for a, c in zip(arr, self._children):
+            a.model_id, a.params, a.nparams = c.model_id, c._params.ctypes.data, c._params.size
+        return arr
+
+    def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
+                 rgb=None, pdf=None, stream=None, mode=3):
+        torch = _torch()
+        ix, iy, iz, n = _soa(in_, what="in")
+        ox, oy, oz, _ = _soa(out, n, what="out")
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        if mode & 1:
+            rgb = torch.empty((3, n), dtype=torch.float32, device=dev) if rgb is None else \
+                _out_rows(rgb, 3, n, dev, "rgb")
+        if mode & 2:
+            pdf = torch.empty((n,), dtype=torch.float32, device=dev) if pdf is None else \
+                _out_rows(pdf, 0, n, dev, "pdf")
+        _on_stream(stream, _keep, rgb, pdf)
+        d = self._desc()
+        _lib.check(_lib.load().bbm_hip_aggregate_eval_pdf(
+            d, len(self._children), ix, iy, iz, ox, oy, oz, mptr, n, int(component), int(unit),
+            rgb[0].data_ptr() if mode & 1 else None, rgb[1].data_ptr() if mode & 1 else None,
+            rgb[2].data_ptr() if mode & 1 else None, pdf.data_ptr() if mode & 2 else None, _stream_ptr(stream)))
+        return rgb, pdf
+
+    eval = BsdfModel.eval
+    pdf = BsdfModel.pdf
+
+    def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
+        torch = _torch()
+        ox, oy, oz, n = _soa(out, what="out")
+        x0, x1 = (xi if isinstance(xi, (tuple, list)) else (xi[0], xi[1]))
+        for x in (x0, x1):
+            if x.dtype != torch.float32 or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
+                raise TypeError("xi: expected float32 CUDA rows with one entry per direction")
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = x0.device
+        d = torch.empty((3, n), dtype=torch.float32, device=dev)
+        p = torch.empty((n,), dtype=torch.float32, device=dev)
+        f = torch.empty((n,), dtype=torch.int32, device=dev)
+        _on_stream(stream, _keep, d, p, f)
+        desc = self._desc()
+        _lib.check(_lib.load().bbm_hip_aggregate_sample(
+            desc, len(self._children), ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component), int(unit),
+            d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(), _stream_ptr(stream)))
+        return BsdfSample(d, p, f)
+
+    def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
+        torch = _torch()
+        ox, oy, oz, n = _soa(out, what="out")
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = (out[0] if isinstance(out, (tuple, list)) else out).device
+        rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
+        _on_stream(stream, _keep, rgb)
+        desc = self._desc()
+        _lib.check(_lib.load().bbm_hip_aggregate_reflectance(
+            desc, len(self._children), ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
+            rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
+        return rgb
+
+
+def Aggregate(*children, fused=True):
+    """aggregate(models...) (aggregatemodel.h:232-233): the fused kernel for the published fits' form
+    Aggregate(Lambertian, X) where one is registered (fused=False forces the composed path), otherwise an
+    AggregateModel over the children's own kernels."""
     key = aggregate_key([c.name for c in children])
-    if key not in AGGREGATES:
-        raise ValueError(f"unsupported aggregate: {key}")
-    return BsdfModel(key, *children)
+    if fused and key in AGGREGATES and all(isinstance(c, BsdfModel) for c in children):
+        return BsdfModel(key, *children)
+    return AggregateModel(*children)
 
 
 def _make_ctor(name):

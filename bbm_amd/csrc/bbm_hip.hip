@@ -185,6 +185,7 @@ const AggregateSpec kAggregates[] = {
   BBM_HIP_AGG("Aggregate<Lambertian,NganLafortune>", "NganLafortune", AggNganLafortuneM),  // fits/ngan_lafortune.fit
   BBM_HIP_AGG("Aggregate<Lambertian,NganWard>", "NganWard", AggNganWardM),                 // fits/ngan_ward.fit
   BBM_HIP_AGG("Aggregate<Lambertian,NganWardDuer>", "NganWardDuer", AggNganWardDuerM),     // fits/ngan_wardduer.fit
+  BBM_HIP_AGG("Aggregate<Lambertian,NganHe>", "NganHe", AggNganHeM),                       // fits/ngan_he.fit
 };
 
 const ModelEntry* single(const char* name)

@@ -11,6 +11,8 @@
 #include "he.hpp"
 #include "merl.hpp"
 
+#include <type_traits>
+
 namespace bbmhip {
 
 // Compositions (reference file:line):
@@ -51,6 +53,25 @@ using AggNganCookTorranceM = Aggregate<Lambertian, NganCookTorranceM>;
 using AggNganLafortuneM = Aggregate<Lambertian, NganLafortuneM>;
 using AggNganWardM = Aggregate<Lambertian, NganWardM>;
 using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
+using AggNganHeM = Aggregate<Lambertian, NganHeM>;    // fits/ngan_he.fit
+
+// An aggregate's per-launch derived data is its children's (the He family's sampling CDF): B's block starts
+// after A's parameters, and B's derived slots (B::kParams + ...) are then exactly the aggregate's own
+// (A::kParams + B::kParams + ...), where B's device constructor (p + A::kParams) finds them.
+template<class A, class B>
+struct host_params<Aggregate<A, B>>
+{
+  static_assert(std::is_same_v<A, Lambertian>, "fused aggregates have a Lambertian first child");
+  static int run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch)
+  {
+    ParamBlock q{};
+    for (int k = A::kParams; k < kMaxParams; ++k) q.v[k - A::kParams] = p.v[k];
+    if (const int rc = host_params<B>::run(q, component, s, scratch)) return rc;
+    for (int k = A::kParams; k < kMaxParams; ++k) p.v[k] = q.v[k - A::kParams];
+    return 0;
+  }
+  static void done(void* scratch, hipStream_t s) { host_params<B>::done(scratch, s); }
+};
 
 }  // namespace bbmhip
 
@@ -68,7 +89,7 @@ using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 #define BBM_HIP_MERL_MODELS(X) X(Merl)
 #define BBM_HIP_AGGREGATE_MODELS(X) \
   X(AggBagherM) X(AggCookTorranceM) X(AggGGXM) X(AggLowASM) X(AggLowMicrofacetM) X(AggLowSmoothM) X(AggNganASM) \
-  X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM)
+  X(AggPhongM) X(AggNganCookTorranceM) X(AggNganLafortuneM) X(AggNganWardM) X(AggNganWardDuerM) X(AggNganHeM)
 
 #define BBM_HIP_INSTANTIATE(M)                                                   \
   template int launch_eval_pdf<M>(const EvalArgs&, int, hipStream_t);           \

@@ -62,7 +62,8 @@ ATTRIBUTES = {
 # form, fits/*.fit).  Parameters are the children's vectors concatenated in order.
 AGGREGATES = {f"Aggregate<Lambertian,{x}>": ("Lambertian", x) for x in (
     "Bagher", "CookTorrance", "GGX", "LowCookTorrance", "LowAshikhminShirley", "LowMicrofacetFit", "LowSmooth",
-    "NganAshikhminShirley", "NganBlinnPhong", "NganCookTorrance", "NganLafortune", "NganWard", "NganWardDuer")}
+    "NganAshikhminShirley", "NganBlinnPhong", "NganCookTorrance", "NganLafortune", "NganWard", "NganWardDuer",
+    "NganHe")}
 
 
 def aggregate_key(children):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 5
+#define BBM_HIP_ABI_VERSION 6
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -117,6 +117,37 @@ int bbm_hip_reflectance(int model_id, const float* params, int nparams,
                         const float* out_x, const float* out_y, const float* out_z,
                         const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
                         float* r, float* g, float* b, void* stream);
+
+/* ---------------------------------------------------------------- aggregates of any models */
+
+/* aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 registered models, each
+ * child given as (model id, its parameter vector): replaces the reference's variadic template instantiation
+ * (aggregatemodel.h:222 `aggregatemodel<MODELS...>`, aggregate() :232-233) for compositions that have no fused
+ * registry entry ("Aggregate<Lambertian,X>").  Evaluated by composing the children's kernels (one pass per
+ * child; eval and reflectance as the reference's right fold, pdf as the reflectance-weighted mixture, sample
+ * by the reference's child selection on xi0).  Same conventions as the single-model entry points; `r` may be
+ * NULL in bbm_hip_aggregate_eval_pdf for pdf only, `pdf` NULL for eval only. */
+typedef struct bbm_hip_child
+{
+  int model_id;
+  const float* params;   /* host memory, nparams floats (bbm_hip_model_nparams) */
+  int nparams;
+} bbm_hip_child;
+
+int bbm_hip_aggregate_eval_pdf(const bbm_hip_child* children, int nchildren,
+                               const float* in_x, const float* in_y, const float* in_z,
+                               const float* out_x, const float* out_y, const float* out_z,
+                               const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                               float* r, float* g, float* b, float* pdf, void* stream);
+int bbm_hip_aggregate_sample(const bbm_hip_child* children, int nchildren,
+                             const float* out_x, const float* out_y, const float* out_z,
+                             const float* xi0, const float* xi1,
+                             const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                             float* dir_x, float* dir_y, float* dir_z, float* pdf, uint32_t* flag, void* stream);
+int bbm_hip_aggregate_reflectance(const bbm_hip_child* children, int nchildren,
+                                  const float* out_x, const float* out_y, const float* out_z,
+                                  const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                                  float* r, float* g, float* b, void* stream);
 
 /* ---------------------------------------------------------------- fitting (BASELINE config 5) */
 

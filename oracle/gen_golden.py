@@ -59,6 +59,7 @@ FIT_FILES = {   # Aggregate(Lambertian, X) -> the published fit used as the 'fit
     "Aggregate<Lambertian,NganLafortune>": "ngan_lafortune.fit",
     "Aggregate<Lambertian,NganWard>": "ngan_ward.fit",
     "Aggregate<Lambertian,NganWardDuer>": "ngan_wardduer.fit",
+    "Aggregate<Lambertian,NganHe>": "ngan_he.fit",
 }
 
 

@@ -48,12 +48,34 @@ template<typename T> using ngancooktorrance_t = bbm::ngancooktorrance<T>;
 template<typename T> using nganlafortune_t = bbm::nganlafortune<T>;
 template<typename T> using nganward_t = bbm::nganward<T>;
 template<typename T> using nganwardduer_t = bbm::nganwardduer<T>;
+template<typename T> using nganhe_t = bbmref::nganhe<T>;
+template<typename T> using lambertian_t = bbm::lambertian<T>;
+template<typename T> using orennayar_t = bbm::orennayar<T>;
+template<typename T> using ward_t = bbm::ward<T>;
+
+// aggregatemodel<X...> of any models (aggregatemodel.h:222): the compositions the GPU evaluates by composing its
+// children's kernels (bbm_hip_aggregate_*), a few of each kind: three children, no Lambertian, a data-driven
+// sampler child (a child type may appear once: the children are the aggregate's base classes)
+template<template<typename> class... X>
+struct aggv
+{
+  using f = bbm::aggregatemodel<X<C>...>;
+  using d = bbm::aggregatemodel<X<CD>...>;
+};
+#define BBMREF_AGGV(KEY, ...) \
+  entry{ KEY, \
+         &ops<typename aggv<__VA_ARGS__>::f>::defaults, &ops<typename aggv<__VA_ARGS__>::f>::bounds, \
+         &ops<typename aggv<__VA_ARGS__>::f>::to_string, \
+         &ops<typename aggv<__VA_ARGS__>::f>::template evalpdf<float>, \
+         &ops<typename aggv<__VA_ARGS__>::d>::template evalpdf<double>, \
+         &ops<typename aggv<__VA_ARGS__>::f>::template sample<float>, &ops<typename aggv<__VA_ARGS__>::f>::reflectance, \
+         &ops<typename aggv<__VA_ARGS__>::f>::from_string }
 
 #define BBMREF_AGG(X, KEY) \
   entry{ KEY, \
          &ops<agg<X>>::defaults, &ops<agg<X>>::bounds, &ops<agg<X>>::to_string, \
          &ops<agg<X>>::template evalpdf<float>, &ops<aggd<X>>::template evalpdf<double>, \
-         &ops<agg<X>>::template sample<float>, &ops<agg<X>>::reflectance }
+         &ops<agg<X>>::template sample<float>, &ops<agg<X>>::reflectance, &ops<agg<X>>::from_string }
 
 const std::vector<entry>& aggregate_registry()
 {
@@ -71,6 +93,10 @@ const std::vector<entry>& aggregate_registry()
     BBMREF_AGG(nganlafortune_t, "Aggregate<Lambertian,NganLafortune>"),            // fits/ngan_lafortune.fit
     BBMREF_AGG(nganward_t, "Aggregate<Lambertian,NganWard>"),                      // fits/ngan_ward.fit
     BBMREF_AGG(nganwardduer_t, "Aggregate<Lambertian,NganWardDuer>"),              // fits/ngan_wardduer.fit
+    BBMREF_AGG(nganhe_t, "Aggregate<Lambertian,NganHe>"),                          // fits/ngan_he.fit
+    BBMREF_AGGV("Aggregate<Lambertian,CookTorrance,GGX>", lambertian_t, cooktorrance_t, ggx_t),
+    BBMREF_AGGV("Aggregate<CookTorrance,GGX>", cooktorrance_t, ggx_t),
+    BBMREF_AGGV("Aggregate<OrenNayar,NganHe,Ward>", orennayar_t, nganhe_t, ward_t),
   };
   return r;
 }
@@ -311,6 +337,10 @@ const std::vector<std::pair<const char*, std::vector<uint32_t> (*)()>>& agg_attr
     BBMREF_AGG_ATTRS(nganlafortune_t, "Aggregate<Lambertian,NganLafortune>"),
     BBMREF_AGG_ATTRS(nganward_t, "Aggregate<Lambertian,NganWard>"),
     BBMREF_AGG_ATTRS(nganwardduer_t, "Aggregate<Lambertian,NganWardDuer>"),
+    BBMREF_AGG_ATTRS(nganhe_t, "Aggregate<Lambertian,NganHe>"),
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "Aggregate<Lambertian,CookTorrance,GGX>", &param_attrs<aggv<lambertian_t, cooktorrance_t, ggx_t>::f> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "Aggregate<CookTorrance,GGX>", &param_attrs<aggv<cooktorrance_t, ggx_t>::f> },
+    std::pair<const char*, std::vector<uint32_t> (*)()>{ "Aggregate<OrenNayar,NganHe,Ward>", &param_attrs<aggv<orennayar_t, nganhe_t, ward_t>::f> },
   };
   return r;
 }

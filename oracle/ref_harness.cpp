@@ -152,6 +152,14 @@ int bbmref_reflectance(const char* name, const float* p, int np, size_t n,
   return 0;
 }
 
+// bbm::fromString of the model `name` (a model string as printed by toString / stored in fits/*.fit) -> its
+// parameter vector (All | Dependent, declaration order); <0 if the reference rejects the string
+int bbmref_from_string(const char* name, const char* str, float* out, int cap)
+{
+  auto e = find(name); if(!e || !e->from_string) return -2;
+  return e->from_string(str, out, cap);
+}
+
 int bbmref_max_threads(void)
 {
 #ifdef _OPENMP

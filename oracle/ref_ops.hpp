@@ -97,6 +97,20 @@ struct ops
     return r;
   }
 
+  // bbm::fromString<M> (include/bbm/bsdf_string_convert.h, aggregatemodel.h:193-218) -> the parameter vector
+  static int from_string(const char* str, float* out, int cap)
+  {
+    try
+    {
+      M m = bbm::fromString<M>(std::string(str));
+      auto pv = bbm::parameter_values(m, kAllParams);
+      int k = 0;
+      for(auto& v : pv) { if(k < cap) out[k] = float(v); ++k; }
+      return k;
+    }
+    catch(const std::exception&) { return -1; }
+  }
+
   static std::string to_string(const float* p, int np)
   {
     M m = make(p, np);
@@ -192,6 +206,7 @@ struct entry
   void (*evalpdf_d)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, int, double*, double*, double*, double*, int);
   void (*sample_f)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*, float*, uint32_t*, int);
   void (*reflectance_f)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*);
+  int (*from_string)(const char*, float*, int) = nullptr;
 };
 
 #define BBMREF_ENTRY(MODEL) BBMREF_ENTRY_NS(bbm, MODEL)
@@ -203,7 +218,8 @@ struct entry
          &ops<NS::MODEL<bbm::floatRGB>>::template evalpdf<float>, \
          &ops<NS::MODEL<bbm::doubleRGB>>::template evalpdf<double>, \
          &ops<NS::MODEL<bbm::floatRGB>>::template sample<float>, \
-         &ops<NS::MODEL<bbm::floatRGB>>::reflectance }
+         &ops<NS::MODEL<bbm::floatRGB>>::reflectance, \
+         &ops<NS::MODEL<bbm::floatRGB>>::from_string }
 
 
 } // namespace bbmref
