@@ -70,6 +70,18 @@ def aggregate_key(children):
     return "Aggregate<" + ",".join(children) + ">"
 
 
+def aggregate_children(name):
+    """Children of an aggregate key: the fused entries' (AGGREGATES) or, for any other `Aggregate<A,B,...>` of
+    single models (the composed path), the names in the key."""
+    if name in AGGREGATES:
+        return AGGREGATES[name]
+    if name.startswith("Aggregate<") and name.endswith(">"):
+        kids = tuple(name[len("Aggregate<"):-1].split(","))
+        if len(kids) >= 2 and all(k in ATTRIBUTES for k in kids):
+            return kids
+    return None
+
+
 def attr_size(shape):
     n = 1
     for d in shape:
@@ -78,8 +90,9 @@ def attr_size(shape):
 
 
 def nparams(name):
-    if name in AGGREGATES:
-        return sum(nparams(c) for c in AGGREGATES[name])
+    kids = aggregate_children(name)
+    if kids is not None:
+        return sum(nparams(c) for c in kids)
     return sum(attr_size(s) for _, s in ATTRIBUTES[name])
 
 
@@ -100,9 +113,10 @@ def fmt_attr(values, shape):
 def to_string(name, params):
     """bbm::toString(model): `Name(attr = value, ...)` in attribute declaration order;
     aggregates print `Aggregate(child, child)` (aggregatemodel.h:168-179)."""
-    if name in AGGREGATES:
+    kids = aggregate_children(name)
+    if kids is not None:
         parts, k = [], 0
-        for c in AGGREGATES[name]:
+        for c in kids:
             n = nparams(c)
             parts.append(to_string(c, params[k:k + n]))
             k += n

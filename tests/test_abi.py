@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 5
+    assert lib.bbm_hip_abi_version() == 6
 
 
 def test_registry_matches_reference(lib):
@@ -64,9 +64,21 @@ def test_registry_matches_reference(lib):
             np.testing.assert_array_equal(np.array(buf[:], np.float32), np.array(ref[key], np.float32), err_msg=f"{name} {key}")
 
 
+def _composed_children(name):
+    """Children of a golden aggregate that has no fused registry entry (composed path, bbm_hip_aggregate_*)."""
+    from bbm_amd.models import AGGREGATES
+    if not name.startswith("Aggregate<") or name in AGGREGATES:
+        return None
+    return name[len("Aggregate<"):-1].split(",")
+
+
 def test_python_mirror_layout_covers_every_reference_model():
     from bbm_amd.models import AGGREGATES, ATTRIBUTES, nparams
     for name, ref in META["models"].items():
+        kids = _composed_children(name)
+        if kids is not None:     # composed aggregate: the children's vectors in order
+            assert all(k in ATTRIBUTES for k in kids) and sum(nparams(k) for k in kids) == ref["nparams"], name
+            continue
         assert name in ATTRIBUTES or name in AGGREGATES, name
         assert nparams(name) == ref["nparams"], name
 
@@ -74,7 +86,15 @@ def test_python_mirror_layout_covers_every_reference_model():
 def test_param_attrs_match_reference(lib):
     """bsdf_attr flags per parameter == what bbm::parameter_values(model, flag) selects in the reference."""
     names = [lib.bbm_hip_model_name(i).decode() for i in range(lib.bbm_hip_num_models())]
-    assert set(names) - {"Merl"} == set(META["models"])
+    composed = {n for n in META["models"] if _composed_children(n) is not None}
+    assert set(names) - {"Merl"} == set(META["models"]) - composed
+    for name in composed:     # an aggregate's flags are its children's, in order
+        flags = []
+        for kid in _composed_children(name):
+            buf = (ctypes.c_uint32 * 64)()
+            k = lib.bbm_hip_model_param_attrs(names.index(kid), buf, 64)
+            flags += [int(buf[j]) for j in range(k)]
+        assert flags == META["models"][name]["attrs"], name
     for i, name in enumerate(names):
         if name == "Merl":        # measured data, no attributes in the reference: tests/test_merl.py
             continue
