@@ -57,6 +57,8 @@ SIGNATURES = {
     "bbm_hip_aggregate_eval_pdf": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
     "bbm_hip_aggregate_sample": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
     "bbm_hip_aggregate_reflectance": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
+    "bbm_hip_model_layout": (ctypes.c_char_p, [_I]),
+    "bbm_hip_parse_model": (_I, [ctypes.c_char_p, _P, _P, _P, _I, _I]),
 }
 
 

@@ -149,6 +149,21 @@ int bbm_hip_aggregate_reflectance(const bbm_hip_child* children, int nchildren,
                                   const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
                                   float* r, float* g, float* b, void* stream);
 
+/* ---------------------------------------------------------------- model strings */
+
+/* Attribute layout of a single model, "name:count,..." in declaration order (the order of its parameter
+ * vector and of toString); NULL for aggregates / unknown ids. */
+const char* bbm_hip_model_layout(int model_id);
+
+/* Parse a model string -- bbm::toString form, an entry of the fits/ files, `Aggregate(child, child, ...)` -- as the
+ * reference's runtime fromString does (include/bbm/bsdf_string_convert.h:52-85; the handle behind bsdf_ptr,
+ * checkBsdf and the Mitsuba plugin).  A single model or an aggregate with a fused kernel yields ONE entry
+ * (model_ids[0], its nparams[0] parameters); any other aggregate yields one entry per child, to be evaluated
+ * with bbm_hip_aggregate_*.  Parameters are written back to back into params.  Returns the number of entries
+ * (>= 1) or an error code (unknown model / attribute, malformed string, value beyond the float range). */
+int bbm_hip_parse_model(const char* str, int* model_ids, float* params, int* nparams, int max_children,
+                        int params_capacity);
+
 /* ---------------------------------------------------------------- fitting (BASELINE config 5) */
 
 /* Linearizer: a bijection between an index range [0, size) and (in, out) direction pairs
