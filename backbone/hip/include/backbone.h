@@ -1,0 +1,79 @@
+/* backbone/hip/include/backbone.h -- BBM_BACKBONE=hip: the backbone header bbm/bbm_core.h:10 includes.
+ *
+ * A BBM backbone supplies the lane types every bsdfmodel<CONF> is written against (Value, Spectrum, vec2d/vec3d,
+ * complex, masks, rng) and the named configurations (include/core/backbone.h:34-49 validates them through
+ * BBM_VALIDATE_BACKBONE when a model imports its config, bbm/config.h:31-40).  The HIP backbone is split by where
+ * the work runs:
+ *
+ *   - per-lane host code (constructors, attribute reflection, toString/fromString, the reference's own scalar
+ *     eval used by checkBsdf's CPU statistics and by tests) keeps scalar lanes: the lane types are the scalar
+ *     ones of the native backbone (backbone/native/include/backbone/*.h, second on the include path, see
+ *     backbone.cmake), so every model header compiles and every config passes BBM_VALIDATE_BACKBONE unchanged;
+ *   - batched work (eval / pdf / sample / reflectance over N directions, the fitting loss) goes to the GPU through
+ *     bbm_hip/batch.h (bbm::hip::eval_pdf(model, ...), ..., bbm::hip::loss_sums) and libbbm_hip (include/bbm_hip.h).
+ *     The batch entry points take any model instance of the reference's template API or a runtime bsdf_ptr.
+ *
+ * So the lane width of this backbone is 1 on the host and N on the device: there is no packet config (the
+ * enoki/drjit backbones' floatPacketRGB), because the device batch IS the packet, laid out SoA in HBM.
+ *
+ * Configurations (backbone.cmake BBM_BACKBONE_CONFIGURATIONS): floatRGB (device kernels compute in f32 with the
+ * native backbone's rounding) and doubleRGB (host only: the device adapter static_asserts Value ==
+ * float).
+ */
+#ifndef _BBM_HIP_BACKBONE_H_
+#define _BBM_HIP_BACKBONE_H_
+
+#include "util/string_literal.h"
+
+// scalar lane types and their math, control, horizontal, rng and string conversion (native backbone headers)
+#include "backbone/array.h"
+#include "backbone/complex.h"
+#include "backbone/vec.h"
+#include "backbone/color.h"
+#include "backbone/type_traits.h"
+#include "backbone/control.h"
+#include "backbone/math.h"
+#include "backbone/horizontal.h"
+#include "backbone/random.h"
+#include "backbone/python.h"
+#include "backbone/stringconvert.h"
+
+//! \brief set when the HIP backbone is active (BBM_BACKBONE=hip); bbm_hip/batch.h is then usable
+#define BBM_BACKBONE_HIP 1
+
+namespace bbm {
+
+  namespace hip {
+    /*******************************************************************/
+    /*! \brief Shape of an RGB configuration of the HIP backbone.
+
+      \tparam LANE = host lane type (float / double scalar)
+      \tparam LABEL = configuration name (reported by bbm_info, used by the python export)
+      \tparam SELF = the configuration struct itself (CRTP; bbm::get_config<T> = T::Config)
+
+      Spectrum is the native 3-channel color; wavelength() gives the channel centres in micron that the
+      complex-Fresnel and Bagher models read (fresnel_complex.h) -- the device kernels are compiled with the
+      same three values (bbm_amd/csrc/he.hpp kWavelength).
+    ********************************************************************/
+    template<typename LANE, string_literal LABEL, typename SELF>
+      struct rgb_config
+    {
+      using Config = SELF;
+      using Value = LANE;
+      using Spectrum = backbone::color<LANE>;
+      static constexpr string_literal name = LABEL;
+
+      //! \brief the device kernels evaluate this configuration (f32 lanes only)
+      static constexpr bool device_batch = std::is_same_v<LANE, float>;
+
+      static Spectrum wavelength(void) { return {0.645, 0.526, 0.444}; }
+    };
+  } // end hip namespace
+
+  /*** The configurations of this backbone ***/
+  struct floatRGB : public hip::rgb_config<float, "floatRGB", floatRGB> {};
+  struct doubleRGB : public hip::rgb_config<double, "doubleRGB", doubleRGB> {};
+
+} // end bbm namespace
+
+#endif /* _BBM_HIP_BACKBONE_H_ */

@@ -1,30 +1,41 @@
-/* backbone/hip/include/bbm_hip/batch.h -- C++20 host adapter: bbm::bsdfmodel<> -> libbbm_hip.
+/* backbone/hip/include/bbm_hip/batch.h -- C++20 host adapter: bbm::bsdfmodel<> / bsdf_ptr -> libbbm_hip.
  *
- * Header-only, compiled by the BBM user's host compiler (g++/clang) together with the BBM headers;
- * it never includes HIP device code.  A model instance of the reference's template API, e.g.
+ * Header-only, compiled by the BBM user's host compiler (g++/clang) together with the BBM headers and the HIP
+ * backbone (backbone/hip/include/backbone.h, selected by BBM_BACKBONE=hip); it never includes HIP device code.
+ * A model instance of the reference's template API, e.g.
  *
  *     bbm::cooktorrance<bbm::floatRGB> ct;             // include/bsdfmodel/cooktorrance.h:28-34
  *     bbm::hip::eval_pdf(ct, in, out, n, rgb, pdf);     // N pairs on the GPU
  *
  * is mapped to the HIP backbone in two steps:
- *   1. its *type* is matched against the compositions the kernels implement (cooktorrance<C>,
- *      ggx<C>, lambertian<C>, ...) -- a composition the GPU does not implement is a compile error,
- *      never a silent fallback;
+ *   1. its *type* is matched against the compositions the kernels implement (cooktorrance<C>, ggx<C>,
+ *      lambertian<C>, the He family and Merl behind their data-driven sampler, aggregatemodel<...>) -- a
+ *      composition the GPU does not implement is a compile error, never a silent fallback;
  *   2. its attributes are packed with bbm::parameter_values(model, All | Dependent)
  *      (include/bbm/bsdf_enumerate.h), i.e. in declaration order, and passed by value.
- * Device buffers are caller-owned SoA float arrays; calls are asynchronous on `stream`.
- * Errors from the C-ABI are rethrown as bbm::hip::error (a std::runtime_error), matching the
- * reference's exception style (include/core/error.h:42-46).
+ * The runtime handle bsdf_ptr<C> (include/bbm/bsdf_ptr.h:21-165, what checkBsdf and the Mitsuba plugin hold)
+ * is mapped through its toString() and the library's parser of the reference's model strings
+ * (bbm_hip_parse_model): a single model or fused aggregate runs its kernel, any other aggregate (including the
+ * runtime aggregatebsdf) runs composed from its children's kernels (bbm_hip_aggregate_*).
+ * Device buffers are caller-owned SoA float arrays; calls are asynchronous on `stream`.  Errors from the C-ABI
+ * are rethrown as bbm::hip::error (a std::runtime_error), matching the reference's exception style
+ * (include/core/error.h:42-46).
  */
 #ifndef BBM_HIP_BATCH_H
 #define BBM_HIP_BATCH_H
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "bbm/bsdf_enumerate.h"
 #include "bbm_hip.h"
@@ -49,8 +60,66 @@ namespace bbm {
       if(rc < 0) throw error(rc, bbm_hip_last_error());
     }
 
+    inline int id_of(const std::string& name)
+    {
+      const int i = bbm_hip_model_id(name.c_str());
+      check(i);
+      return i;
+    }
+
     namespace detail {
       template<typename T> struct dependent_false : std::false_type {};
+
+#ifdef _BBM_HE_H_
+      //! \brief the he_base<...> (he.h:115-482) a type derives from, with its policy arguments
+      template<typename T> struct he_params { static constexpr bool value = false; };
+      template<typename C, typename F, bbm::he_eq25 A, bbm::he_eq78 B, size_t NR, size_t TT, bool AD, auto RA, auto NM>
+        struct he_params<bbm::he_base<C, F, A, B, NR, TT, AD, RA, NM>>
+      {
+        static constexpr bool value = true;
+        using base = bbm::he_base<C, F, A, B, NR, TT, AD, RA, NM>;
+        static constexpr bool complex_fresnel = std::is_same_v<F, bbm::fresnel::complex<C, bbm::Spectrum_t<C>>>;
+        static constexpr bool cook_fresnel = std::is_same_v<F, bbm::fresnel::cook<C>>;
+        static constexpr bool errata = (A == bbm::he_eq25::Errata), westin = (B == bbm::he_eq78::Westin);
+        static constexpr size_t newton = NR, taylor = TT;
+        static constexpr bool adaptive = AD;
+        static constexpr double approx = double(RA.value);
+      };
+      template<typename C, typename F, bbm::he_eq25 A, bbm::he_eq78 B, size_t NR, size_t TT, bool AD, auto RA, auto NM>
+        he_params<bbm::he_base<C, F, A, B, NR, TT, AD, RA, NM>> he_base_of(const bbm::he_base<C, F, A, B, NR, TT, AD, RA, NM>*);
+      he_params<void> he_base_of(...);
+
+      //! \brief registry name of a He-family model: he_base with the policy arguments of he.h:489-496 (or ngan.h:166
+      //! for "NganHe*", which the library exposes only with its specular scale), wrapped in the data-driven
+      //! backscatter sampler (a bare he_base has no importance sampler of its own and is rejected); nullptr if
+      //! W is none of them
+      template<typename W>
+        constexpr const char* he_name()
+      {
+        using P = decltype(he_base_of(static_cast<const W*>(nullptr)));
+        if constexpr (!P::value) return nullptr;
+        else if constexpr (std::is_same_v<W, typename P::base> || P::newton != 4) return nullptr;
+        else if constexpr (P::complex_fresnel && !P::errata && !P::westin && P::taylor == 64 && P::adaptive && P::approx == 18.0) return "He";
+        else if constexpr (P::complex_fresnel && P::errata && P::westin && P::taylor == 64 && P::adaptive && P::approx == 18.0) return "HeWestin";
+        else if constexpr (P::complex_fresnel && P::errata && !P::westin && P::taylor == 10 && !P::adaptive) return "HeHolzschuch";
+        else if constexpr (P::cook_fresnel && P::errata && P::westin && P::taylor == 64 && P::adaptive && P::approx == 18.0) return "NganHe*";
+        else return nullptr;
+      }
+#endif
+
+#ifdef _BBM_MERL_H_
+      //! \brief merl_data<C, NAME> (staticmodel/merl.h:38-221) a type derives from
+      template<typename C, auto NM> std::true_type merl_probe(const bbm::merl_data<C, NM>*);
+      std::false_type merl_probe(...);
+      template<typename C, auto NM> bbm::merl_data<C, NM> merl_base_of(const bbm::merl_data<C, NM>*);
+#endif
+
+#if defined(_BBM_NDF_EPD_H_) && defined(_BBM_MASKINGSHADOWING_VANGINNEKEN_H_)
+      template<typename M> struct is_epd : std::false_type {};
+      template<typename C, auto NM>
+        struct is_epd<bbm::microfacet<bbm::ndf::epd<C>, bbm::maskingshadowing::vanginneken<C>, bbm::fresnel::complex<C>,
+                                      bbm::microfacet_n::Walter, NM>> : std::true_type {};
+#endif
 
       //! \brief Registry name of the GPU kernel implementing MODEL's composition.
       template<typename MODEL>
@@ -154,108 +223,332 @@ namespace bbm {
         if constexpr (std::is_same_v<M, bbm::bagher<C>>) return "Bagher";
         else
 #endif
-#ifdef _BBM_HOLZSCHUCHPACANOWSKI_H_
-        if constexpr (std::is_same_v<M, bbm::epd<C>>) return "EPD";
+#if defined(_BBM_NDF_EPD_H_) && defined(_BBM_MASKINGSHADOWING_VANGINNEKEN_H_)
+        // EPD (holzschuchpacanowski.h:34-42) by its composition: the alias's normalisation argument is unused there
+        if constexpr (is_epd<M>::value) return "EPD";
+        else
+#endif
+#ifdef _BBM_HE_H_
+        // He, HeWestin, HeHolzschuch: ndf_sampler<he_base<...>, 90, 1, NAME> (he.h:489-496)
+        if constexpr (he_name<M>() != nullptr && he_name<M>()[0] == 'H') return he_name<M>();
+        else
+#endif
+#ifdef _BBM_MERL_H_
+        // Merl (merl.h:224-225): the registry entry; its parameters (the table) come from the file, see describe()
+        if constexpr (decltype(merl_probe(static_cast<const M*>(nullptr)))::value) return "Merl";
         else
 #endif
         static_assert(dependent_false<M>::value, "this bsdfmodel composition has no HIP kernel (see DESIGN.md)");
         return nullptr;
       }
 
-#ifdef _BBM_AGGREGATEMODEL_H_
-      //! \brief aggregatemodel<lambertian<C>, X> (include/bsdfmodel/aggregatemodel.h:222): the form of every
-      //! published fit; the kernel is registered as "Aggregate<Lambertian,X>"
-      template<typename M> struct lambertian_aggregate : std::false_type {};
-      template<typename C, typename X>
-        struct lambertian_aggregate<bbm::aggregatemodel<bbm::lambertian<C>, X>> : std::true_type { using child = X; };
+#ifdef _BBM_SCALED_MODEL_H_
+      //! \brief NganHe = scaledmodel<ndf_sampler<he_base<CONF, cook, Errata, Westin, 4, 64, true, 18>, 90, 1,
+      //! "NganHe">, SpecularScale> (ngan.h:166-167)
+      template<typename M> struct scaled_he { static constexpr bool value = false; };
+#ifdef _BBM_HE_H_
+      template<typename W>
+        struct scaled_he<bbm::scaledmodel<W, bbm::bsdf_attr::SpecularScale>>
+      {
+        static constexpr bool value = he_name<W>() != nullptr && he_name<W>()[0] == 'N';
+      };
+#endif
 #else
-      template<typename M> struct lambertian_aggregate : std::false_type {};
+      template<typename M> struct scaled_he { static constexpr bool value = false; };
 #endif
 
-      //! \brief Registry name of MODEL's kernel (single models and Aggregate(Lambertian, X))
+#ifdef _BBM_AGGREGATEMODEL_H_
+      //! \brief aggregatemodel_base<NAME, MODELS...> (aggregatemodel.h:22-214): its children, in order
+      template<typename M> struct aggregate_of { static constexpr bool value = false; };
+      template<auto NM, typename... X>
+        struct aggregate_of<bbm::aggregatemodel_base<NM, X...>> { static constexpr bool value = true; using children = std::tuple<X...>; };
+#else
+      template<typename M> struct aggregate_of { static constexpr bool value = false; };
+#endif
+
+      //! \brief calls f.template operator()<X>() for every type of a std::tuple<X...> (no instance is built)
+      template<typename F, typename... X>
+        inline void for_each_type(F&& f, const std::tuple<X...>*) { (f.template operator()<X>(), ...); }
+
+      //! \brief single-kernel registry name of MODEL (single models; Aggregate<A,B,...> names the fused entry
+      //! when the library has one, e.g. "Aggregate<Lambertian,NganHe>")
       template<typename MODEL>
-        inline std::string registry_name()
+        inline std::string single_name()
       {
         using M = std::decay_t<MODEL>;
-        if constexpr (lambertian_aggregate<M>::value)
-          return std::string("Aggregate<Lambertian,") + gpu_name<typename lambertian_aggregate<M>::child>() + ">";
+        if constexpr (scaled_he<M>::value) return "NganHe";
+        else if constexpr (aggregate_of<M>::value)
+        {
+          std::string key;
+          for_each_type([&]<typename X>() { key += (key.empty() ? "Aggregate<" : ",") + single_name<X>(); },
+                        static_cast<const typename aggregate_of<M>::children*>(nullptr));
+          return key + ">";
+        }
         else return gpu_name<M>();
       }
     } // end detail namespace
 
-    //! \brief libbbm_hip model id of MODEL (resolved once per type)
-    template<typename MODEL>
-      inline int model_id()
-    {
-      static const int id = [] { int i = bbm_hip_model_id(detail::registry_name<MODEL>().c_str()); check(i); return i; }();
-      return id;
-    }
-
-    //! \brief Flat parameter vector of a model instance (attribute declaration order)
+    //! \brief Flat parameter vector of a model instance (attribute declaration order, All | Dependent)
     template<typename MODEL>
       inline std::vector<float> parameters(const MODEL& model)
     {
       std::vector<float> p;
-      for(auto& v : bbm::parameter_values(model, bsdf_attr(0x1F))) p.push_back(float(v));   // All | Dependent
+      for(auto& v : bbm::parameter_values(model, bsdf_attr(0x1F))) p.push_back(float(v));
       return p;
     }
 
-    //! \brief eval + pdf of N (in, out) pairs (bsdfmodel::eval / ::pdf batched)
-    template<typename MODEL>
-      inline void eval_pdf(const MODEL& model, soa3 in, soa3 out, size_t n, soa3_out rgb, float* pdf,
-                           bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
-                           const uint8_t* mask=nullptr, void* stream=nullptr)
+#ifdef _BBM_MERL_H_
+    namespace detail {
+      //! \brief device float4 table of a MERL file (bbm_hip_merl_table), built once per file and kept for the
+      //! process's lifetime (the Merl model's parameters are its address)
+      inline const float* merl_device_table(const std::string& filename)
+      {
+        static std::mutex mu;
+        static std::map<std::string, void*> tables;
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = tables.find(filename);
+        if(it != tables.end()) return static_cast<const float*>(it->second);
+        std::ifstream f(filename, std::ios::binary);
+        if(!f) throw error(BBM_HIP_ERR_INVALID_ARG, "unable to open MERL BRDF: " + filename);
+        uint32_t dims[3];
+        f.read(reinterpret_cast<char*>(dims), sizeof(dims));
+        const size_t n = size_t(dims[0]) * dims[1] * dims[2];
+        if(!f || n != BBM_HIP_MERL_ENTRIES) throw error(BBM_HIP_ERR_INVALID_ARG, "not a recognized MERL BRDF: " + filename);
+        std::vector<double> raw(3 * n);
+        f.read(reinterpret_cast<char*>(raw.data()), std::streamsize(raw.size() * sizeof(double)));
+        if(!f) throw error(BBM_HIP_ERR_INVALID_ARG, "truncated MERL BRDF: " + filename);
+        void* draw = nullptr;
+        void* table = nullptr;
+        if(hipMalloc(&draw, raw.size() * sizeof(double)) != hipSuccess || hipMalloc(&table, n * 16) != hipSuccess)
+          throw error(BBM_HIP_ERR_HIP, "hipMalloc failed for the MERL table");
+        if(hipMemcpy(draw, raw.data(), raw.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+          throw error(BBM_HIP_ERR_HIP, "hipMemcpy failed for the MERL table");
+        check(bbm_hip_merl_table(static_cast<const double*>(draw), dims[0], dims[1], dims[2], static_cast<float*>(table), nullptr));
+        if(hipDeviceSynchronize() != hipSuccess) throw error(BBM_HIP_ERR_HIP, "MERL table build failed");
+        (void)hipFree(draw);
+        tables[filename] = table;
+        return static_cast<const float*>(table);
+      }
+
+      //! \brief filename of a merl_data model from its toString, Merl("...") (merl.h:161-164)
+      inline std::string merl_filename(const std::string& s)
+      {
+        const size_t a = s.find('"'), b = s.rfind('"');
+        if(a == std::string::npos || b <= a) throw error(BBM_HIP_ERR_INVALID_ARG, "not a Merl model string: " + s);
+        return s.substr(a + 1, b - a - 1);
+      }
+    } // end detail namespace
+#endif
+
+    //! \brief A model as the library sees it: one registry entry (single model / fused aggregate) or the
+    //! children of a composed aggregate, each with its parameter vector.
+    struct model_desc
     {
-      auto p = parameters(model);
-      check(bbm_hip_eval_pdf(model_id<MODEL>(), p.data(), int(p.size()), in.x, in.y, in.z, out.x, out.y, out.z,
-                             mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, pdf, stream));
+      std::vector<int> ids;
+      std::vector<std::vector<float>> params;
+      bool composed(void) const { return ids.size() > 1; }
+      std::vector<bbm_hip_child> children(void) const
+      {
+        std::vector<bbm_hip_child> c(ids.size());
+        for(size_t k = 0; k < ids.size(); ++k) c[k] = {ids[k], params[k].data(), int(params[k].size())};
+        return c;
+      }
+    };
+
+    //! \brief model_desc of a model string (bsdf_ptr toString, a fits/ entry) via the library's parser
+    inline model_desc from_string(const std::string& s)
+    {
+#ifdef _BBM_MERL_H_
+      if(s.rfind("Merl(", 0) == 0)
+      {
+        const float* t = detail::merl_device_table(detail::merl_filename(s));
+        const uint64_t v = reinterpret_cast<uint64_t>(t);
+        const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+        std::vector<float> p(2);
+        std::memcpy(&p[0], &lo, 4);
+        std::memcpy(&p[1], &hi, 4);
+        return model_desc{{id_of("Merl")}, {p}};
+      }
+#endif
+      std::vector<int> ids(64), np(64);
+      std::vector<float> buf(64 * 64);
+      const int k = bbm_hip_parse_model(s.c_str(), ids.data(), buf.data(), np.data(), 64, int(buf.size()));
+      check(k);
+      model_desc d;
+      size_t off = 0;
+      for(int c = 0; c < k; ++c)
+      {
+        d.ids.push_back(ids[size_t(c)]);
+        d.params.emplace_back(buf.begin() + long(off), buf.begin() + long(off + size_t(np[size_t(c)])));
+        off += size_t(np[size_t(c)]);
+      }
+      return d;
+    }
+
+    //! \brief model_desc of a model instance, resolved by type (compile-time dispatch)
+    template<typename MODEL>
+      inline model_desc describe(const MODEL& model)
+    {
+      using M = std::decay_t<MODEL>;
+#ifdef _BBM_MERL_H_
+      // Merl: ndf_sampler<merl_data<C, "Merl">, 90, 1> (staticmodel/merl.h:224-225), identified by its file
+      // (toString, merl.h:161-164); a bare merl_data (placeholder sampler, merl.h:108-115) is rejected
+      if constexpr (!detail::scaled_he<M>::value && !detail::aggregate_of<M>::value &&
+                    decltype(detail::merl_probe(static_cast<const M*>(nullptr)))::value)
+      {
+        static_assert(!std::is_same_v<M, decltype(detail::merl_base_of(static_cast<const M*>(nullptr)))>,
+                      "merl_data without its data-driven sampler has no HIP kernel; use bbm::merl<CONF>");
+        return from_string(bbm::toString(model));
+      }
+      else
+#endif
+      if constexpr (detail::aggregate_of<M>::value)
+      {
+        const std::string key = detail::single_name<M>();
+        const int fused = bbm_hip_model_id(key.c_str());
+        if(fused >= 0) return model_desc{{fused}, {parameters(model)}};
+        // composed: each child (a base class of the aggregate) with its own kernel and parameters
+        model_desc d;
+        detail::for_each_type([&]<typename X>() {
+          const model_desc c = describe(static_cast<const X&>(model));
+          if(c.composed()) throw error(BBM_HIP_ERR_UNSUPPORTED, "nested aggregates are not supported");
+          d.ids.push_back(c.ids[0]);
+          d.params.push_back(c.params[0]);
+        }, static_cast<const typename detail::aggregate_of<M>::children*>(nullptr));
+        return d;
+      }
+      else return model_desc{{id_of(detail::single_name<M>())}, {parameters(model)}};
+    }
+
+#ifdef _BBM_BSDF_PTR_H_
+    //! \brief bsdf_ptr<C> (include/bbm/bsdf_ptr.h:21-165): through its toString (bsdf.h:111-116 pipes the
+    //! wrapped model's) and the library's parser
+    template<typename C>
+      inline model_desc describe(const bbm::bsdf_ptr<C>& ptr) { return from_string(ptr.toString()); }
+#endif
+
+    //! \brief libbbm_hip model id of MODEL's single kernel (resolved once per type)
+    template<typename MODEL>
+      inline int model_id()
+    {
+      static const int id = id_of(detail::single_name<MODEL>());
+      return id;
+    }
+
+    //! \brief eval + pdf of N (in, out) pairs (bsdfmodel::eval / ::pdf batched)
+    inline void eval_pdf(const model_desc& m, soa3 in, soa3 out, size_t n, soa3_out rgb, float* pdf,
+                         bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                         const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const auto c = m.children();
+        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+                                         uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, pdf, stream));
+      }
+      else
+        check(bbm_hip_eval_pdf(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+                               out.z, mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, pdf, stream));
     }
 
     //! \brief eval of N (in, out) pairs -> RGB
+    inline void eval(const model_desc& m, soa3 in, soa3 out, size_t n, soa3_out rgb,
+                     bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                     const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const auto c = m.children();
+        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+                                         uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, nullptr, stream));
+      }
+      else
+        check(bbm_hip_eval(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+                           out.z, mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+    }
+
+    //! \brief pdf of N (in, out) pairs
+    inline void pdf(const model_desc& m, soa3 in, soa3 out, size_t n, float* pdf,
+                    bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                    const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const auto c = m.children();
+        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+                                         uint32_t(component), uint32_t(unit), nullptr, nullptr, nullptr, pdf, stream));
+      }
+      else
+        check(bbm_hip_pdf(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+                          out.z, mask, n, uint32_t(component), uint32_t(unit), pdf, stream));
+    }
+
+    //! \brief sample N (out, xi) -> BsdfSample{direction, pdf, flag} (bsdfmodel::sample batched)
+    inline void sample(const model_desc& m, soa3 out, const float* xi0, const float* xi1, size_t n,
+                       soa3_out direction, float* pdf, uint32_t* flag,
+                       bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                       const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const auto c = m.children();
+        check(bbm_hip_aggregate_sample(c.data(), int(c.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
+                                       uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf,
+                                       flag, stream));
+      }
+      else
+        check(bbm_hip_sample(m.ids[0], m.params[0].data(), int(m.params[0].size()), out.x, out.y, out.z, xi0, xi1, mask,
+                             n, uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf, flag,
+                             stream));
+    }
+
+    //! \brief reflectance of N out directions -> RGB (bsdfmodel::reflectance batched)
+    inline void reflectance(const model_desc& m, soa3 out, size_t n, soa3_out rgb,
+                            bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                            const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const auto c = m.children();
+        check(bbm_hip_aggregate_reflectance(c.data(), int(c.size()), out.x, out.y, out.z, mask, n, uint32_t(component),
+                                            uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+      }
+      else
+        check(bbm_hip_reflectance(m.ids[0], m.params[0].data(), int(m.params[0].size()), out.x, out.y, out.z, mask, n,
+                                  uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+    }
+
+    // The same entry points on a model instance (template API) or a bsdf_ptr: resolved, then dispatched.
+    template<typename MODEL>
+      inline void eval_pdf(const MODEL& model, soa3 in, soa3 out, size_t n, soa3_out rgb, float* p,
+                           bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                           const uint8_t* mask=nullptr, void* stream=nullptr)
+    { eval_pdf(describe(model), in, out, n, rgb, p, component, unit, mask, stream); }
+
     template<typename MODEL>
       inline void eval(const MODEL& model, soa3 in, soa3 out, size_t n, soa3_out rgb,
                        bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                        const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      auto p = parameters(model);
-      check(bbm_hip_eval(model_id<MODEL>(), p.data(), int(p.size()), in.x, in.y, in.z, out.x, out.y, out.z,
-                         mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
-    }
+    { eval(describe(model), in, out, n, rgb, component, unit, mask, stream); }
 
-    //! \brief pdf of N (in, out) pairs
     template<typename MODEL>
-      inline void pdf(const MODEL& model, soa3 in, soa3 out, size_t n, float* pdf,
+      inline void pdf(const MODEL& model, soa3 in, soa3 out, size_t n, float* p,
                       bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                       const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      auto p = parameters(model);
-      check(bbm_hip_pdf(model_id<MODEL>(), p.data(), int(p.size()), in.x, in.y, in.z, out.x, out.y, out.z,
-                        mask, n, uint32_t(component), uint32_t(unit), pdf, stream));
-    }
+    { pdf(describe(model), in, out, n, p, component, unit, mask, stream); }
 
-    //! \brief sample N (out, xi) -> BsdfSample{direction, pdf, flag} (bsdfmodel::sample batched)
     template<typename MODEL>
       inline void sample(const MODEL& model, soa3 out, const float* xi0, const float* xi1, size_t n,
-                         soa3_out direction, float* pdf, uint32_t* flag,
+                         soa3_out direction, float* p, uint32_t* flag,
                          bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                          const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      auto p = parameters(model);
-      check(bbm_hip_sample(model_id<MODEL>(), p.data(), int(p.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
-                           uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf, flag,
-                           stream));
-    }
+    { sample(describe(model), out, xi0, xi1, n, direction, p, flag, component, unit, mask, stream); }
 
-    //! \brief reflectance of N out directions -> RGB (bsdfmodel::reflectance batched)
     template<typename MODEL>
       inline void reflectance(const MODEL& model, soa3 out, size_t n, soa3_out rgb,
                               bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                               const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      auto p = parameters(model);
-      check(bbm_hip_reflectance(model_id<MODEL>(), p.data(), int(p.size()), out.x, out.y, out.z, mask, n,
-                                uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
-    }
+    { reflectance(describe(model), out, n, rgb, component, unit, mask, stream); }
 
     //! \brief Sample losses of include/loss/*.h, for loss_sums
     enum class loss_t : int { nganL2 = BBM_LOSS_NGAN_L2, lowL2 = BBM_LOSS_LOW_L2, bieronL2 = BBM_LOSS_BIERON_L2,
@@ -265,7 +558,8 @@ namespace bbm {
     //! for nprobes parameter vectors of MODEL's type at once (device array nprobes x parameters(model).size(),
     //! e.g. the 2P probes of a compass step), over n materialised pairs with reference values ref:
     //! sums[p] = sum_i loss(model(probes[p]).eval(in_i, out_i), ref_i) in double (device).  Divide by the
-    //! linearizer size (after summing the shards of all GPUs) for the reference's loss value.
+    //! linearizer size (after summing the shards of all GPUs) for the reference's loss value.  MODEL must have a
+    //! single kernel (single model or fused aggregate).
     template<typename MODEL>
       inline void loss_sums(const MODEL& model, const float* probes, int nprobes, soa3 in, soa3 out, size_t n,
                             soa3 ref, loss_t loss, double* sums, void* workspace, size_t workspace_bytes,
