@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -21,6 +22,64 @@ int fail(int code, const std::string& msg)
 {
   g_last_error = msg;
   return code;
+}
+
+// ------------------------------------------------------------------------ stream-ordered scratch
+
+namespace {
+struct ScratchBlock
+{
+  void* p;
+  size_t bytes;
+  int device;
+  hipEvent_t released;     // recorded on `last` when the block was released
+  hipStream_t last;
+  bool busy, used;
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchBlock> g_scratch;
+}  // namespace
+
+void* scratch_acquire(size_t bytes, hipStream_t s)
+{
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  bytes = (bytes + 255) & ~size_t(255);
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  ScratchBlock* best = nullptr;
+  for (ScratchBlock& b : g_scratch)
+    if (!b.busy && b.device == dev && b.bytes >= bytes && (!best || b.bytes < best->bytes)) best = &b;
+  if (best)
+  {
+    // its last user's work must be done before this stream writes it: free on the same stream (stream
+    // order), otherwise a GPU-side wait on the release event
+    if (best->used && best->last != s && hipStreamWaitEvent(s, best->released, 0) != hipSuccess) return nullptr;
+    best->busy = true;
+    return best->p;
+  }
+  ScratchBlock b{nullptr, bytes, dev, nullptr, s, true, false};
+  if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&b.released, hipEventDisableTiming) != hipSuccess)
+  {
+    (void)hipFree(b.p);
+    return nullptr;
+  }
+  g_scratch.push_back(b);
+  return b.p;
+}
+
+void scratch_release(void* p, hipStream_t s)
+{
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  for (ScratchBlock& b : g_scratch)
+    if (b.p == p)
+    {
+      (void)hipEventRecord(b.released, s);
+      b.last = s;
+      b.busy = false;
+      b.used = true;
+      return;
+    }
 }
 
 BBM_HIP_MICROFACET_MODELS(BBM_HIP_EXTERN)

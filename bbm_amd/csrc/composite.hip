@@ -13,7 +13,7 @@
 //   reflectance = MODELS::reflectance(...) + ...  (right fold)                                       (:156-163)
 // Each child runs through the public entry points (its registry kernel, its own host-side preparation such as
 // the He family's CDF); the small kernels below only combine per-lane results in the reference's order and
-// rounding.  Scratch is stream-ordered (hipMallocAsync / hipFreeAsync): no host synchronisation.
+// rounding.  Scratch is stream-ordered (scratch_acquire / scratch_release): no host synchronisation.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -25,6 +25,8 @@
 
 namespace bbmhip {
 int fail(int code, const std::string& msg);
+void* scratch_acquire(size_t bytes, hipStream_t s);
+void scratch_release(void* p, hipStream_t s);
 
 namespace {
 
@@ -117,12 +119,11 @@ struct Scratch
   hipStream_t s;
   std::vector<void*> ptrs;
   explicit Scratch(hipStream_t st) : s(st) {}
-  ~Scratch() { for (void* p : ptrs) (void)hipFreeAsync(p, s); }
+  ~Scratch() { for (void* p : ptrs) scratch_release(p, s); }
   template<class T> T* get(size_t count)
   {
-    void* p = nullptr;
-    if (hipMallocAsync(&p, (count ? count : 1) * sizeof(T), s) != hipSuccess) return nullptr;
-    ptrs.push_back(p);
+    void* p = scratch_acquire((count ? count : 1) * sizeof(T), s);
+    if (p) ptrs.push_back(p);
     return static_cast<T*>(p);
   }
 };

@@ -11,7 +11,7 @@
 // sample / pdf use a 90-bin CDF over theta_h of the model's own backscatter eval(h, h) (ndf/sampler.h:143-181).
 // That CDF depends on the parameters and the sampled component, so it is built per launch on the GPU
 // (k_he_cdf: 90 evaluations + the serial float prefix sum of util/cdf.h:39-47) into stream-ordered
-// scratch memory whose address travels in the parameter block after the model's parameters; the kernels
+// scratch memory (scratch_acquire) whose address travels in the parameter block after the model's parameters; the kernels
 // read it from there (host_params<He<...>> below).  No host synchronisation.
 #pragma once
 #include "math.hpp"
@@ -255,9 +255,23 @@ struct He
     // within ~2^-20 ulp of a rounding midpoint.  That matters beyond accuracy: the adaptive stop (he.h:460)
     // compares consecutive terms, and near the series' peak they are nearly equal, so terms that differed by
     // an ulp would truncate the series one term early or late where D is tiny.
-    double eg[3];
+    double eg[3], cap[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp_dd(-g[c]);
+    // Exact early exit (adaptive series only).  Past the peak (m + 1 >= g) every later term is at most
+    //   cap * gm_m / m,  cap = e^(-g) e^(-eb/64) (1 + 2^-10)
+    // (g^m'/m'! and 1/m' decrease, eb/m' >= eb/64 up to float rounding, the margin covers gm's per-step
+    // roundings).  Once that bound is below half an ulp of a channel's float sum (below 2^-150 while the sum is
+    // still 0) on all three channels, no later term can change any sum: the loop's only output is final, so
+    // it stops there with exactly the reference's result, wherever the reference's own stop (he.h:459) lies.
+    // Without it, lanes whose terms underflow to 0 (large eb: e^(-eb/m) for small m) never meet the stop
+    // rule (0 < 0 is false) and run all 64 terms -- one such lane in a wave keeps all 64 lanes busy.
+    if (ADAPTIVE)
+    {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        cap[c] = converged ? 0.0 : eg[c] * exp_dd(-double(eb[c]) * (1.0 / 64.0)) * (1.0 + 0x1p-10);
+    }
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);
@@ -279,8 +293,20 @@ struct He
       }
       // converged |= hmin(term) < eps && hmin(term) < hmin(last) (he.h:460)
       if (ADAPTIVE)
+      {
         converged = (fminf(fminf(term[0], term[1]), term[2]) < kEpsF) &&
                     (fminf(fminf(term[0], term[1]), term[2]) < fminf(fminf(last[0], last[1]), last[2]));
+        bool settled = (m & 3) == 0;      // tested every 4th term: the bound costs as much as a third of a term
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+        {
+          // half an ulp of sum[c] (2^-150 for 0 and subnormal sums)
+          const int e = (sum[c] > 0.0f) ? __builtin_amdgcn_frexp_expf(sum[c]) - 25 : -150;
+          const double half_ulp = __builtin_ldexp(1.0, max(e, -150));
+          settled = settled && (double(m) + 1.0 >= g[c]) && (cap[c] * double(gm[c]) * rm < half_ulp);
+        }
+        converged = converged || settled;
+      }
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], rough[c], weight)));
@@ -396,9 +422,9 @@ __global__ __launch_bounds__(128) void k_he_cdf(ParamBlock p, uint32_t component
 template<class M>
 int ndf_sampler_cdf_run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch, const char* who)
 {
-  float* cdf = nullptr;
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&cdf), kHeBins * sizeof(float), s);
-  if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: hipMallocAsync: " + hipGetErrorString(e));
+  float* cdf = static_cast<float*>(scratch_acquire(kHeBins * sizeof(float), s));
+  if (!cdf) return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: scratch allocation failed");
+  hipError_t e;
   hipLaunchKernelGGL((k_he_cdf<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
   if ((e = hipGetLastError()) != hipSuccess)
     return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: launch: " + hipGetErrorString(e));
@@ -416,8 +442,13 @@ struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
   {
     return ndf_sampler_cdf_run<M>(p, component, s, scratch, "He");
   }
-  static void done(void* scratch, hipStream_t s) { if (scratch) (void)hipFreeAsync(scratch, s); }
+  static void done(void* scratch, hipStream_t s) { if (scratch) scratch_release(scratch, s); }
 };
+
+// The He evaluation is VALU-bound (the Taylor series, ~10^3 instructions per pair) and zero outside the upper
+// hemisphere and on masked lanes (eval_rgb / eval_pdf above): evaluate live pairs only, packed densely
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct compact_eval<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr bool value = true; };
 
 // he.h:489-496, ngan.h:166-167
 using HeM = He<FresnelComplexRGB, false, false, 64, true, 18, false>;

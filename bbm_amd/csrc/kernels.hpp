@@ -30,6 +30,15 @@ constexpr int kMaxBlocks = 1 << 22;   // effectively one workgroup per 1024 pair
 // Record `msg` as the calling thread's last error (bbm_hip_last_error) and return `code`.
 int fail(int code, const std::string& msg);
 
+// Stream-ordered device scratch (bbm_hip.hip): per-launch derived data (the tabulated samplers' CDFs) and the
+// composed aggregates' per-lane temporaries.  A released block keeps an event recorded on the releasing
+// stream; re-acquiring it on the same stream needs nothing (stream order), on another stream that stream
+// waits for the event on the GPU.  No host synchronisation; blocks are kept for reuse.  (Replaces
+// hipMallocAsync / hipFreeAsync on the caller's stream, under which tests/cpp/adapter_check -- a plain C++
+// host program on the null stream -- saw He CDFs and composed-aggregate outputs corrupted at random.)
+void* scratch_acquire(size_t bytes, hipStream_t s);
+void scratch_release(void* p, hipStream_t s);
+
 struct ParamBlock { float v[kMaxParams]; };
 
 // Per-model host work before a launch (e.g. building a lookup table on first use); no-op by default.
@@ -268,6 +277,129 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
     one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
 }
 
+// Models whose per-pair eval is VALU-heavy AND returns exactly zero (rgb and pdf) for every pair outside the
+// upper hemisphere (z(in) <= 0 or z(out) <= 0, NaN included) and for masked pairs: those run through
+// k_eval_pdf_compact, which evaluates only the live pairs, packed densely into waves.
+template<class Model> struct compact_eval { static constexpr bool value = false; };
+
+// Compaction on/off (BBM_HIP_COMPACT=0 disables; A/B experiments).
+inline bool use_compact()
+{
+  static const bool v = [] {
+    const char* e = std::getenv("BBM_HIP_COMPACT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// Stream compaction of live pairs before evaluation.  A wave executes the slowest of its 64 lanes: for a
+// VALU-bound model (the He series) a wave of uniformly random sphere pairs spends 3/4 of its lanes on pairs
+// that only ever produce 0 (both directions must be in the upper hemisphere) yet pay for the full evaluation
+// in lock step with the live ones.  Here each workgroup takes a tile of 1024 pairs (4 per thread, the same
+// 16-byte loads as k_eval_pdf_v4), writes the live ones' directions densely into LDS (wave prefix sum +
+// per-wave offsets), evaluates them one per lane -- every wave but the last fully occupied -- and writes the
+// results back into the LDS slot they came from; the owner threads then store all four outputs (zeros for
+// dead pairs) with 16-byte streaming stores.  The evaluation is the model's own eval_pdf on the same
+// operands, so the results are bit-identical to the uncompacted kernels.  LDS: 24 KiB per workgroup.
+template<class Model, int MODE, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_compact(EvalArgs a)
+{
+  constexpr int kTile = 4 * kBlock;
+  __shared__ float job[6][kTile];      // live pairs' in.xyz, out.xyz; rows 0..3 then hold rgb, pdf
+  __shared__ int wave_total[kBlock / 64];
+  const Model m(a.p.v);
+  const uint64_t n4 = a.n >> 2;
+  const uint64_t tiles = (n4 + kBlock - 1) / kBlock;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x)
+  {
+    const uint64_t t = tile * kBlock + threadIdx.x;
+    const bool have = t < n4;
+    float4 ix{}, iy{}, iz{}, ox{}, oy{}, oz{};
+    uint32_t mk = 0;
+    if (have)
+    {
+      ix = ld4<true>(a.ix, t); iy = ld4<true>(a.iy, t); iz = ld4<true>(a.iz, t);
+      ox = ld4<true>(a.ox, t); oy = ld4<true>(a.oy, t); oz = ld4<true>(a.oz, t);
+      mk = MASK ? reinterpret_cast<const uint32_t*>(a.mask)[t] : 0x01010101u;
+    }
+    const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
+    const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
+    bool live[4];
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      live[j] = ((mk >> (8 * j)) & 0xffu) && (inz[j] > 0) && (onz[j] > 0);
+      cnt += live[j];
+    }
+    // inclusive prefix sum of the live counts over the wave
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+      const int v = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += v;
+    }
+    if (lane == 63) wave_total[wave] = incl;
+    __syncthreads();
+    int base = incl - cnt, total = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w)
+    {
+      const int tw = wave_total[w];
+      base += (w < wave) ? tw : 0;
+      total += tw;
+    }
+    int slot[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+    {
+      slot[j] = base;
+      if (live[j])
+      {
+        job[0][base] = inx[j]; job[1][base] = iny[j]; job[2][base] = inz[j];
+        job[3][base] = onx[j]; job[4][base] = ony[j]; job[5][base] = onz[j];
+        ++base;
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < total; q += kBlock)
+    {
+      float rgb[3], pdf;
+      m.template eval_pdf<MODE>(mk3(job[0][q], job[1][q], job[2][q]), mk3(job[3][q], job[4][q], job[5][q]),
+                                a.component, rgb, pdf);
+      job[0][q] = rgb[0]; job[1][q] = rgb[1]; job[2][q] = rgb[2]; job[3][q] = pdf;
+    }
+    __syncthreads();
+    if (have)
+    {
+      float r[4], g[4], b[4], p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+      {
+        r[j] = live[j] ? job[0][slot[j]] : 0.0f;
+        g[j] = live[j] ? job[1][slot[j]] : 0.0f;
+        b[j] = live[j] ? job[2][slot[j]] : 0.0f;
+        p[j] = live[j] ? job[3][slot[j]] : 0.0f;
+      }
+      if (MODE & kModeEval)
+      {
+        st4<true>(a.r, t, r[0], r[1], r[2], r[3]);
+        st4<true>(a.g, t, g[0], g[1], g[2], g[3]);
+        st4<true>(a.b, t, b[0], b[1], b[2], b[3]);
+      }
+      if (MODE & kModePdf) st4<true>(a.pdf, t, p[0], p[1], p[2], p[3]);
+    }
+    __syncthreads();     // the next tile reuses job[] and wave_total[]
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
+  {
+    const uint64_t i = (n4 << 2) + threadIdx.x;
+    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+  }
+}
+
 // Grid cap for the grid-stride kernels; BBM_HIP_MAX_BLOCKS overrides it (tuning experiments).
 inline uint64_t max_blocks()
 {
@@ -413,7 +545,9 @@ int launch_mode(const EvalArgs& a0, hipStream_t s)
   else if (vec && !use_nt()) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, false>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else
 #endif
-  if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  if (vec && compact_eval<Model>::value && use_compact())
+    hipLaunchKernelGGL((k_eval_pdf_compact<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));

@@ -135,7 +135,7 @@ struct host_params<Merl>
   {
     return ndf_sampler_cdf_run<Merl>(p, component, s, scratch, "Merl");
   }
-  static void done(void* scratch, hipStream_t s) { if (scratch) (void)hipFreeAsync(scratch, s); }
+  static void done(void* scratch, hipStream_t s) { if (scratch) scratch_release(scratch, s); }
 };
 
 // merl_data::import (merl.h:173-206): channel c of entry i is max(0, raw[c * size + i] * w_c / 1500.0) in

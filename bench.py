@@ -63,6 +63,8 @@ def parse(argv=None):
                     help="weak: --pairs per GPU; strong: --pairs in total, split over the ranks")
     ap.add_argument("--pairs", type=int, default=100_000_000, help="pairs per GPU (weak) or in total (strong)")
     ap.add_argument("--model", default="CookTorrance")
+    ap.add_argument("--models", default=None, help="comma-separated subset of models for --workload models|sample "
+                                                   "(counter passes profile one model at a time)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "selftest"],

@@ -32,6 +32,44 @@ from tools import bench_harness as bh
 SEED = 0xBB5EED
 HBM_PEAK_GBS = 8000.0
 Z_ONLY = {"Lambertian"}
+# f32 vector peak (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs x one wave64 VALU instruction per 2 cycles x 2.4 GHz
+# = 1.2288e12 wave-instructions/s = 78.6e12 lane-instructions/s = 157.3 TFLOP/s counting an FMA as 2 flops
+VALU_PEAK_TFLOPS = 157.3
+VALU_LANE_INSTR_PEAK = VALU_PEAK_TFLOPS * 1e12 / 2
+PMC_VALU_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_valu.json")
+
+
+def _subset(args, names):
+    if not args.models:
+        return list(names)
+    want = [m.strip() for m in args.models.split(",") if m.strip()]
+    return [m for m in names if m in want]
+
+
+def valu_roofline(key, kernel_ms, units):
+    """VALU roofline of one workload's dominant kernel: its VALU instructions per unit come from the committed
+    counter summary (profiles/pmc_valu.json, tools/valu_roofline.py: SQ_INSTS_VALU x 64 lanes / units per
+    dispatch, collected by tools/gpu_pmc_workload.sh), its time from this run's HIP events.  achieved = issued
+    lane-instructions/s x 2 (an FMA's two flops: the unit the 157.3 TFLOP/s f32 vector peak is quoted in), so
+    frac = the fraction of the chip's VALU issue slots this kernel fills (an upper bound on its FLOP fraction)."""
+    entry = None
+    if os.path.exists(PMC_VALU_FILE):
+        try:
+            with open(PMC_VALU_FILE) as f:
+                entry = json.load(f).get("workloads", {}).get(key)
+        except (OSError, ValueError):
+            entry = None
+    if not entry:
+        return {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None,
+                "traffic": None, "kernel_ms": kernel_ms, "note": f"no VALU counter summary for {key}"}
+    per_unit = entry["valu_lane_instr_per_unit"]
+    lane_rate = per_unit * units / (kernel_ms * 1e-3)
+    achieved = 2 * lane_rate / 1e12
+    return {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / VALU_PEAK_TFLOPS, "traffic": None, "kernel": entry.get("kernel"),
+            "kernel_ms": kernel_ms, "valu_instr_per_unit": per_unit,
+            "valu_active_lane_frac": entry.get("valu_active_lane_frac"),
+            "counters": f"profiles/pmc_valu.json[{key}] ({entry.get('source', '')})"}
 
 
 def _timed(step, args, dist, stream):
@@ -56,7 +94,7 @@ def bench_models(args, dist, rank, world):
     stream = torch.cuda.current_stream()
     per = {}
     total_t = 0.0
-    names = [m for m in bbm_amd.model_names() if not m.startswith("Aggregate")]
+    names = _subset(args, [m for m in bbm_amd.model_names() if not m.startswith("Aggregate")])
     for name in names:
         m = _merl_from(bbm_amd.CookTorrance()) if name == "Merl" else bbm_amd.BsdfModel(name)
         elapsed, kern_ms = _timed(lambda: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=stream), args, dist, stream)
@@ -81,7 +119,7 @@ def bench_sample(args, dist, rank, world):
     stream = torch.cuda.current_stream()
     res = {}
     total_t = 0.0
-    for name in ("CookTorrance", "GGX"):
+    for name in _subset(args, ("CookTorrance", "GGX")):
         m = bbm_amd.BsdfModel(name)
         d = check.CheckDesc()
         d.test, d.nslots, d.seed, d.begin, d.n = check.REFLECTANCE, slots, SEED, rank * (per_gpu // slots), per_gpu // slots
@@ -101,16 +139,19 @@ def bench_sample(args, dist, rank, world):
         est = a[:, :3] / float(total // slots)
         refl = m.reflectance(outs).cpu().numpy().T
         res[name] = {"samples_per_s": total * args.steps / elapsed, "kernel_ms": kern_ms,
+                     "samples_per_dispatch": (per_gpu // slots) * slots,
+                     "roofline": valu_roofline(f"sample:{name}", kern_ms, (per_gpu // slots) * slots),
                      "estimate_vs_reflectance": [[float(x) for x in est[k]] + [float(y) for y in refl[k]] for k in (0, slots - 1)]}
         total_t += elapsed
     if rank == 0:
-        tot = 2 * (per_gpu // slots) * slots * world * args.steps
+        tot = len(res) * (per_gpu // slots) * slots * world * args.steps
         _line(args, world, "importance-sample->eval->pdf samples/s, microfacet (CookTorrance, GGX), 125M samples per GPU "
-              "(config 4)", tot / total_t, "samples/s", total_t / 2,
+              "(config 4)", tot / total_t, "samples/s", total_t / len(res),
               {"workload": f"checkBsdf reflectance test, importance sampling, {slots} theta_out x "
                            f"{per_gpu // slots} samples per GPU, in-kernel reduction",
                "samples_per_gpu": per_gpu, "parallelism": f"dp{world} (sample shards, one gather at the end)"},
-              {"scaling": "weak", "per_model": res, "roofline": {"bound": "valu", "note": "no per-sample HBM traffic"}})
+              {"scaling": "weak", "per_model": res,
+               "roofline": res.get("CookTorrance", next(iter(res.values())))["roofline"]})
 
 
 def _merl_from(source):
@@ -147,7 +188,9 @@ def bench_fit(args, dist, rank, world):
                            "reference = Merl model read from a synthetic MERL .binary",
                "probes": len(probes), "pairs": pairs, "parallelism": f"dp{world} (grid shards, all-reduce of "
                                                                       f"{len(probes)} doubles per step)"},
-              {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms})
+              {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms,
+               "probe_pairs_per_dispatch": len(probes) * (pairs // world),
+               "roofline": valu_roofline("fit:Aggregate<Lambertian,Bagher>", kern_ms, len(probes) * (pairs // world))})
 
 
 def run(args, dist, rank, world):

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSVs for one kernel: per-dispatch counter sums (median over dispatches).
 
-    python tools/pmc_summary.py gpurun_out/pmc2 k_eval_pdf_v4
+    python tools/pmc_summary.py gpurun_out/pmc2 k_eval_pdf_v4            # {counter: median, dispatch_ns: ...}
+    python tools/pmc_summary.py --by-kernel gpurun_out/pmc2 k_check      # {kernel name: {counter: median, ...}}
+
+`root` holds one sub-directory per counter pass (rocprofv3 -d <root>/<pass>); every *counter_collection.csv
+below a pass directory is read.
 """
 import collections
 import csv
@@ -12,25 +16,33 @@ import statistics
 import sys
 
 
-def summarise(root, pattern):
-    out = {}
-    for f in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv"))):
-        per = collections.defaultdict(float)
-        dur = {}
-        for r in csv.DictReader(open(f)):
-            if pattern not in r["Kernel_Name"]:
+def _rows(root):
+    for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
+        yield f, csv.DictReader(open(f))
+
+
+def summarise(root, pattern, by_kernel=False):
+    per = collections.defaultdict(float)            # (kernel, file, dispatch, counter) -> sum over dimensions
+    dur = collections.defaultdict(dict)              # kernel -> {(file, dispatch): ns}
+    for f, rows in _rows(root):
+        for r in rows:
+            k = r["Kernel_Name"]
+            if pattern not in k:
                 continue
-            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-            dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        byc = collections.defaultdict(list)
-        for (d, c), v in per.items():
-            byc[c].append(v)
-        for c, v in byc.items():
-            out[c] = statistics.median(v)
-        if dur:
-            out.setdefault("dispatch_ns", statistics.median(dur.values()))
-    return out
+            kk = k if by_kernel else pattern
+            per[(kk, f, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+            dur[kk][(f, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    byc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (kk, _, _, c), v in per.items():
+        byc[kk][c].append(v)
+    out = {}
+    for kk, cs in byc.items():
+        out[kk] = {c: statistics.median(v) for c, v in cs.items()}
+        out[kk]["dispatch_ns"] = statistics.median(dur[kk].values())
+        out[kk]["dispatches"] = len(dur[kk])
+    return out if by_kernel else out.get(pattern, {})
 
 
 if __name__ == "__main__":
-    print(json.dumps(summarise(sys.argv[1], sys.argv[2]), indent=1))
+    args = [a for a in sys.argv[1:] if a != "--by-kernel"]
+    print(json.dumps(summarise(args[0], args[1], by_kernel="--by-kernel" in sys.argv), indent=1))
