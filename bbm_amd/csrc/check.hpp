@@ -107,7 +107,10 @@ __device__ __forceinline__ void wave_reduce_check(double* acc)
 }
 
 template<class Model, int TEST>
-__global__ __launch_bounds__(kBlock) void k_check(CheckArgs a)
+#ifndef BBM_HIP_CHECK_WAVES
+#define BBM_HIP_CHECK_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BBM_HIP_CHECK_WAVES, 8))) void k_check(CheckArgs a)
 {
   __shared__ double part[kBlock / 64][kCheckAcc];
   const Model m(a.p.v);

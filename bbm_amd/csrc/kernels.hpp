@@ -109,8 +109,14 @@ __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, floa
 #define BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_num_sgpr(BBM_HIP_SGPR_LIMIT)))
 #endif
 
+// Minimum waves per SIMD the eval kernels are compiled for (amdgpu_waves_per_eu: caps the VGPRs at 512 / N); 1 =
+// the compiler's choice.  Raised per model where a VALU-bound evaluation would otherwise hold two or three waves
+// per SIMD (too few to hide the f64 / transcendental latencies).
+template<class Model> struct eval_waves { static constexpr int value = 1; };
+
 template<class Model, int MODE, bool MASK, bool NT>
-__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v4(EvalArgs a)
+__global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_waves_per_eu(eval_waves<Model>::value, 8)))
+void k_eval_pdf_v4(EvalArgs a)
 {
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
@@ -301,8 +307,16 @@ inline bool use_compact()
 // results back into the LDS slot they came from; the owner threads then store all four outputs (zeros for
 // dead pairs) with 16-byte streaming stores.  The evaluation is the model's own eval_pdf on the same
 // operands, so the results are bit-identical to the uncompacted kernels.  LDS: 24 KiB per workgroup.
+// Occupancy of the compaction kernel: at least 4 waves per SIMD (<= 128 VGPRs; the He evaluation alone would take
+// 165 -> 3 waves).  Measured on HeWestin / He / HeHolzschuch (10M pairs, tools/gpu_ab_he.sh): 3 waves 1.76 / 1.18 /
+// 0.60 ms, 4 waves 1.48 / 0.97 / 0.58, 5 waves 1.50 / 1.00 / 0.67, 6 waves 1.52 / 1.01 / 0.68 -- the few spilled
+// dwords cost less than the latency the fourth wave hides.
+#ifndef BBM_HIP_COMPACT_WAVES
+#define BBM_HIP_COMPACT_WAVES 4
+#endif
+#define BBM_HIP_COMPACT_ATTR __attribute__((amdgpu_waves_per_eu(BBM_HIP_COMPACT_WAVES, 8)))
 template<class Model, int MODE, bool MASK>
-__global__ __launch_bounds__(kBlock) void k_eval_pdf_compact(EvalArgs a)
+__global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compact(EvalArgs a)
 {
   constexpr int kTile = 4 * kBlock;
   __shared__ float job[6][kTile];      // live pairs' in.xyz, out.xyz; rows 0..3 then hold rgb, pdf
@@ -679,8 +693,16 @@ __device__ __forceinline__ double wave_sum(double v)
   return v;
 }
 
+// Minimum waves per SIMD of the loss kernel (the probe-batch loop holds ~230 VGPRs unconstrained: 2 waves).
+// Measured on config 5 (Aggregate(Lambertian, Bagher), 36 probes x the MERL grid, tools/gpu_ab_work.sh):
+// 0.87 / 0.73 / 0.62 / 0.61 / 1.09 ms per compass step at 2 / 3 / 4 / 5 / 6 waves.  The He family keeps the
+// compiler's choice (its series would spill heavily at 128 VGPRs; see models.hpp).
+#ifndef BBM_HIP_LOSS_WAVES
+#define BBM_HIP_LOSS_WAVES 4
+#endif
+template<class Model> struct loss_waves { static constexpr int value = BBM_HIP_LOSS_WAVES; };
 template<class Model>
-__global__ __launch_bounds__(kBlock) void k_loss(LossArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_waves<Model>::value, 8))) void k_loss(LossArgs a)
 {
   static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
   __shared__ double part[kBlock / 64][kProbeBatch];

@@ -15,6 +15,22 @@
 
 namespace bbmhip {
 
+// Launch traits of the eval kernels (kernels.hpp), specialised here where every model type is complete.
+// Aggregate(Lambertian, X) is zero outside the upper hemisphere and on masked lanes whenever X is (Lambertian's
+// eval and pdf both need z(in), z(out) > 0), so it shares X's compaction and occupancy choices.
+template<class B> struct compact_eval<Aggregate<Lambertian, B>> { static constexpr bool value = compact_eval<B>::value; };
+template<class B> struct eval_waves<Aggregate<Lambertian, B>> { static constexpr int value = eval_waves<B>::value; };
+template<class B> struct loss_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_waves<B>::value; };
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
+// Bagher's evaluation holds ~180 VGPRs (two waves per SIMD) unconstrained.  Measured (10M pairs, eval+pdf,
+// tools/gpu_ab_he.sh): Bagher 0.238 / 0.203 / 0.262 ms and Aggregate(Lambertian, Bagher) 0.266 / 0.231 / 0.324 ms
+// at 2 / 3 / 4 waves per SIMD -- three it is.
+#ifndef BBM_HIP_BAGHER_WAVES
+#define BBM_HIP_BAGHER_WAVES 3
+#endif
+template<> struct eval_waves<Bagher> { static constexpr int value = BBM_HIP_BAGHER_WAVES; };
+
 // Compositions (reference file:line):
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;         // bsdfmodel/cooktorrance.h:28-34
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                        // bsdfmodel/ggx.h:27-33
