@@ -190,7 +190,7 @@ def bench_fit(args, dist, rank, world):
                                                                       f"{len(probes)} doubles per step)"},
               {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms,
                "probe_pairs_per_dispatch": len(probes) * (pairs // world),
-               "roofline": valu_roofline("fit:Aggregate<Lambertian,Bagher>", kern_ms, len(probes) * (pairs // world))})
+               "roofline": valu_roofline("fit:Aggregate", kern_ms, len(probes) * (pairs // world))})
 
 
 def run(args, dist, rank, world):
