@@ -80,22 +80,21 @@ __device__ __forceinline__ float div_nr(float n, float d)
 // scales by 2^n with v_ldexp_f32 (one rounding, subnormals kept; the kernels run with f32 denormals enabled).
 constexpr float kLn2F = 0.693147180559945309f;
 
-// 2^f for |f| <= ~0.5 in double: Taylor series of e^(f ln2) to degree 11 (|f ln2| <= 0.347: remainder < 2^-44)
+// 2^f for |f| <= 0.5 in double: 1 + f q(f), q a degree-8 polynomial fitted to (2^f - 1) / f on Chebyshev nodes
+// of [-0.5, 0.5] (weighted for relative error): max relative error 2^-45.7 with double Horner, measured over 4e5
+// points -- 9 f64 FMAs where the degree-11 Taylor series of e^(f ln2) took 12 and a multiply.  2^0 = 1 exactly.
 __device__ __forceinline__ double exp2_poly(double f)
 {
-  const double u = f * 0.6931471805599453094;
-  double p = 2.505210838544171877e-08;                           // 1/11!
-  p = __builtin_fma(p, u, 2.755731922398589065e-07);
-  p = __builtin_fma(p, u, 2.755731922398589065e-06);
-  p = __builtin_fma(p, u, 2.480158730158730159e-05);
-  p = __builtin_fma(p, u, 1.984126984126984127e-04);
-  p = __builtin_fma(p, u, 1.388888888888888889e-03);
-  p = __builtin_fma(p, u, 8.333333333333333333e-03);
-  p = __builtin_fma(p, u, 4.166666666666666667e-02);
-  p = __builtin_fma(p, u, 1.666666666666666667e-01);
-  p = __builtin_fma(p, u, 0.5);
-  p = __builtin_fma(p, u, 1.0);
-  return __builtin_fma(p, u, 1.0);
+  double p = 1.013635714986865e-07;
+  p = __builtin_fma(p, f, 1.3258369625240471e-06);
+  p = __builtin_fma(p, f, 1.5253063845032086e-05);
+  p = __builtin_fma(p, f, 0.00015403440667862952);
+  p = __builtin_fma(p, f, 0.0013333557468222406);
+  p = __builtin_fma(p, f, 0.009618129181589533);
+  p = __builtin_fma(p, f, 0.055504108669737956);
+  p = __builtin_fma(p, f, 0.24022650695720274);
+  p = __builtin_fma(p, f, 0.6931471805598511);
+  return __builtin_fma(p, f, 1.0);
 }
 
 // e^a in double for a in [-700, 700], to ~2^-44 relative (exp2_poly and an exact scaling)

@@ -82,7 +82,11 @@ def cpu_baseline(model, din, dout, seconds):
     n = min(din.shape[1], 8_000_000)
     hin = np.ascontiguousarray(din[:, :n].cpu().numpy())
     hout = np.ascontiguousarray(dout[:, :n].cpu().numpy())
-    threads, phys, smt, quota, cpu_model = bh.cpu_topology()
+    aff, phys, smt, quota, cpu_model = bh.cpu_topology()
+    # every CPU this process may use: the affinity mask, capped by the cgroup's CPU quota when there is one (the
+    # GPU box grants 16 CPUs of a 256-thread host: 256 OpenMP threads under that quota were throttled to 1/6 of
+    # the 16-thread rate, profiles/r02_bench_cpu256.json)
+    threads = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
     params = model.parameter_values()
     if ou.ref() is not None:
         kind, fn = "reference", ou.ref_eval_pdf
@@ -97,11 +101,12 @@ def cpu_baseline(model, din, dout, seconds):
         if el >= seconds:
             break
     return {"value": done / el, "unit": "pairs/s", "cores": threads, "kind": kind,
-            "physical_cores": phys, "smt_threads_per_core": smt, "cgroup_cpu_quota": quota,
+            "affinity_threads": aff, "physical_cores": phys, "smt_threads_per_core": smt, "cgroup_cpu_quota": quota,
             "sample": f"{n} pairs of the same synthetic batch, {done // n} passes in {el:.1f} s, "
                       f"{model.name} eval+pdf via {'oracle/_ref (reference headers, native floatRGB)' if kind == 'reference' else 'oracle/port'}, "
-                      f"OpenMP {threads} threads (all threads in this process's affinity mask: {phys} physical "
-                      f"cores x {smt} SMT{'' if quota is None else f'; cgroup CPU quota {quota:g} CPUs'}) on {cpu_model}"}
+                      f"OpenMP {threads} threads = every CPU this process may use (affinity mask: {aff} threads on "
+                      f"{phys} physical cores x {smt} SMT{'' if quota is None else f'; cgroup CPU quota {quota:g} CPUs'}) "
+                      f"on {cpu_model}"}
 
 
 def selftest(args, dist, rank, world):
