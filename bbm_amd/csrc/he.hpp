@@ -56,6 +56,10 @@ __device__ __forceinline__ float std_lerpf(float a, float b, float t)
 // ndf::sampler<NDF, 90, 1> (include/ndf/sampler.h), the data-driven importance sampler bbm::ndf_sampler
 // wraps around the He family and Merl (bbm/ndf_sampler.h:22-164), over a per-launch 90-bin CDF:
 // ndf::sampler::pdf (ndf/sampler.h:102-128) of the halfway vector m
+// theta is the reference's (spherical::theta: a double asin rounded to float): the bin weight w is ~45 x more
+// sensitive to it than the pdf is, and adjacent bins can differ severalfold, so a 2-ulp float asin moved pdfs by
+// ~2e-5.  sin(theta) enters only the Jacobian, as a factor: |m.xy| (~2 ulp from the sine of the float theta, m
+// unit) replaces the correctly rounded sincos.
 __device__ __forceinline__ float ndf_sampler_pdf(const float* __restrict__ cdf, v3 m)
 {
   const float theta = theta_of(m);
@@ -67,9 +71,8 @@ __device__ __forceinline__ float ndf_sampler_pdf(const float* __restrict__ cdf, 
   const int uidx = (ce < 0) ? kHeBins - 1 : min(int(ce), kHeBins - 1);
   auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0f); };
   const float p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
-  float st, ct;
-  cossin_cr(theta, ct, st);
-  const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * fabsf(st)) * kPi2F;
+  const float st = sqrtf(m.x * m.x + m.y * m.y);
+  const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * st) * kPi2F;
   return ((m.z > 0) && (jac > kEpsF)) ? div_nr(p, jac) : 0.0f;
 }
 
