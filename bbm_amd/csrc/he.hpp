@@ -205,7 +205,9 @@ struct He
     const float Ki = (ti > kEpsF) ? K(ti) : 0.0f;
     const float Ko = (to > kEpsF) ? K(to) : 0.0f;
     const float f0 = div_nr(1.0f, sqrtf(kPi8F)) * (Ki + Ko);
-    float x = (f0 <= 1.0f) ? f0 : float(safe_sqrt(2.0 * double(logf_cr(f0))));
+    // safe_sqrt(2.0 * log(f0)): 2 x a float is exact in float and double alike, and a correctly rounded double
+    // sqrt rounded to float is the correctly rounded float sqrt (53 >= 2 x 24 + 2): identical, without the f64 sqrt
+    float x = (f0 <= 1.0f) ? f0 : safe_sqrtf(2.0f * logf_cr(f0));
 #pragma unroll
     for (int s = 0; s < 4; ++s)
     {
@@ -325,7 +327,9 @@ struct He
     const float S = S1(in) * S1(out);
     const float Gv = G(in, out);
     D(in, out, Dv);
-    const float cth = float(safe_sqrt(double(1 + dot3(in, out)) / 2.0));
+    // float(safe_sqrt(double(1 + dot) / 2.0)): halving the float sum is exact in float (1 + dot >= 2^-24 or 0),
+    // and the double-then-float sqrt equals the float sqrt (53 >= 2 x 24 + 2)
+    const float cth = safe_sqrtf((1 + dot3(in, out)) * 0.5f);
     fres.eval3(cth, F);
     const float nrm = div_nr(1.0f, (kPiF * in.z) * out.z);
 #pragma unroll

@@ -121,3 +121,37 @@ def test_composed_equals_fused_for_the_fits_form(bbm):
         assert torch.equal(fs.flag, cs.flag) and torch.equal(fs.direction, cs.direction), x
         assert ou.parity_ok(cs.pdf.cpu().numpy(), fs.pdf.cpu().numpy()).all(), x
         assert torch.equal(fused.reflectance(dout), composed.reflectance(dout)), x
+
+
+def test_scratch_reuse_across_streams(bbm):
+    """The stream-ordered scratch pool (bbm_hip.hip scratch_acquire / scratch_release): composed aggregates and
+    He CDFs issued alternately on two streams, without host synchronisation between them, give exactly the
+    results of the same calls issued one at a time (a block released on one stream and re-acquired on the other
+    is waited for on the GPU)."""
+    n = 1 << 18
+    din = bbm.fill_directions(11, 0, 0, n, mode=1)
+    dout = bbm.fill_directions(11, 1, 0, n, mode=1)
+    torch.cuda.synchronize()
+    models = [bbm.Aggregate(bbm.CookTorrance(), bbm.GGX(), fused=False),
+              bbm.Aggregate(bbm.OrenNayar(), bbm.BsdfModel("NganHe"), bbm.Ward(), fused=False),
+              bbm.BsdfModel("HeWestin")]
+    want = []
+    for m in models:
+        rgb, pdf = m.eval_pdf(din, dout)
+        torch.cuda.synchronize()
+        want.append((rgb.clone(), pdf.clone(), m.reflectance(dout).clone()))
+        torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+    got = []
+    for rep in range(3):
+        for k, m in enumerate(models):
+            s = streams[(rep + k) % 2]
+            with torch.cuda.stream(s):
+                rgb, pdf = m.eval_pdf(din, dout, stream=s)
+                refl = m.reflectance(dout, stream=s)
+            got.append((k, rgb, pdf, refl, s))
+    torch.cuda.synchronize()
+    for k, rgb, pdf, refl, _ in got:
+        assert torch.equal(rgb, want[k][0]) and torch.equal(pdf, want[k][1]) and torch.equal(refl, want[k][2]), k
