@@ -81,6 +81,15 @@ class Merl(BsdfModel):
         ptr = self.table.data_ptr()
         self._params = np.array([ptr & 0xFFFFFFFF, ptr >> 32], dtype=np.uint32).view(np.float32)
 
+    def _pptr(self):
+        # the parameters are the table's device address: valid only on the device that holds it (and only while
+        # this object, which owns the table, is alive -- the C-ABI and C++ callers' contract as well)
+        torch = _torch()
+        if torch.cuda.current_device() != self.table.device.index:
+            raise RuntimeError(f"Merl table lives on cuda:{self.table.device.index}, current device is "
+                               f"cuda:{torch.cuda.current_device()}")
+        return super()._pptr()
+
     def set_parameter_values(self, values):
         raise TypeError("Merl has no settable parameters (measured data)")
 
