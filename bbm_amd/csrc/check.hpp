@@ -138,12 +138,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BBM_HIP_
     if constexpr (TEST == kCheckReflectance)
     {
       v3 dir; float pdf; uint32_t flag;
-      if (a.importance) m.sample(sd, u0, u1, kFlagAll, dir, pdf, flag);
+      float f[3], unused;
+      bool fused = false;
+      if (a.importance)
+      {
+        if constexpr (requires { Model::kFusedSampleEval; })
+        {
+          m.sample_eval(sd, u0, u1, kFlagAll, dir, f, pdf, flag);    // eval(dir, sd) and pdf(dir, sd) at once
+          fused = true;
+        }
+        else m.sample(sd, u0, u1, kFlagAll, dir, pdf, flag);
+      }
       else { dir = sphere_dir(u0, u1, false); pdf = kInv4PiF; }
       if (pdf > kEpsF)
       {
-        float f[3], unused;
-        m.template eval_pdf<kModeEval>(dir, sd, kFlagAll, f, unused);
+        if (!fused) m.template eval_pdf<kModeEval>(dir, sd, kFlagAll, f, unused);
 #pragma unroll
         for (int c = 0; c < 3; ++c) acc[c] += double(div_nr(f[c] * dir.z, pdf));
         acc[3] += 1.0;

@@ -517,6 +517,28 @@ struct Microfacet
     eval_pdf<kModePdf>(dir, out, component, rgb, pdf);
     flag = kFlagSpecular;
   }
+
+  // sample() followed by eval(dir, out): the sample's pdf IS pdf(dir, out) (microfacet.h:135), so one fused
+  // eval_pdf at the sampled direction returns both -- one halfway vector and one D instead of two, results
+  // bit-identical to the separate calls (the fused kernel's contract, tests/test_gpu_parity.py).  checkBsdf's
+  // importance-sampled reflectance (config 4) uses it.
+  static constexpr bool kFusedSampleEval = true;
+  __device__ __forceinline__ void sample_eval(v3 out, float xi0, float xi1, uint32_t component, v3& dir, float* rgb,
+                                              float& pdf, uint32_t& flag) const
+  {
+    dir = mk3(0.0f, 0.0f, 0.0f);
+    pdf = 0.0f;
+    flag = kFlagNone;
+    rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    if (!(component & kFlagSpecular)) return;
+    if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
+    if (!(out.z > 0)) return;
+    const v3 m = ndf.sample(out, xi0, xi1);
+    const float d = dot3(m, out);
+    dir = mk3(2.0f * (m.x * d) - out.x, 2.0f * (m.y * d) - out.y, 2.0f * (m.z * d) - out.z);
+    eval_pdf<kModeEvalPdf>(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
 };
 
 }  // namespace bbmhip
