@@ -113,3 +113,30 @@ def test_sampler_pdf_restatement_matches_reference():
             bs = ou.oracle_eval_pdf(name, p, hb, hb, nthreads=8)
             want = ou.sampler_pdf(ou.sampler_cdf(bs[:3]), ou.golden_inputs()["pin"], ou.golden_inputs()["pout"])
             assert ou.parity_ok(want, g[f"evalpdf{si}"][3]).all(), f"{name}[{si}]"
+
+
+def test_config1_lambertian_native_cpu_1m_pairs():
+    """BASELINE.json configs[0]: Lambertian eval on the native CPU backbone over 1M (in, out) pairs -- the
+    plumbing case without a GPU.  The reference itself (oracle/_ref, native floatRGB) and the C restatement
+    agree bit for bit, and both equal albedo / pi on the upper hemisphere (lambertian.h:45-59)."""
+    import time
+    rng = np.random.default_rng(20240601)
+    n = 1_000_000
+
+    def dirs(sphere):
+        z = (2 * rng.random(n) - 1 if sphere else rng.random(n)).astype(np.float32)
+        ph = (2 * np.pi * rng.random(n)).astype(np.float32)
+        s = np.sqrt(np.maximum(1 - z * z, 0)).astype(np.float32)
+        return np.ascontiguousarray(np.stack([s * np.cos(ph), s * np.sin(ph), z]).astype(np.float32))
+
+    din, dout = dirs(True), dirs(True)
+    albedo = np.float32([0.5, 0.25, 0.125])
+    t0 = time.perf_counter()
+    got = ou.oracle_eval_pdf("Lambertian", albedo, din, dout, nthreads=4)
+    el = time.perf_counter() - t0
+    port = ou.port_eval_pdf("Lambertian", albedo, din, dout, nthreads=4)
+    np.testing.assert_array_equal(got, port)
+    up = (din[2] > 0) & (dout[2] > 0)
+    want = np.where(up, (albedo[:, None] / np.float32(np.pi)).astype(np.float32), np.float32(0))
+    np.testing.assert_array_equal(got[:3], want)
+    assert el < 60, el
