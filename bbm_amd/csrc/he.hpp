@@ -277,6 +277,9 @@ struct He
       for (int c = 0; c < 3; ++c)
         cap[c] = converged ? 0.0 : eg[c] * exp_dd(-double(eb[c]) * (1.0 / 64.0)) * (1.0 + 0x1p-10);
     }
+#ifdef BBM_HIP_HE_PROBE_NO_SERIES
+    converged = true;       // timing probe only (tools/build_variant.sh): the prelude without the series
+#endif
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);
