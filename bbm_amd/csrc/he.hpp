@@ -97,6 +97,14 @@ __device__ __forceinline__ v3 ndf_sampler_halfway(const float* __restrict__ cdf,
   return sph_to_vec(phi, theta);
 }
 
+// ln x for the early-exit bound: exact exponent (frexp, subnormals included) + v_log_f32 of the mantissa, ~1e-7
+// absolute; -inf for 0 (a zero gm or g makes every later term 0)
+__device__ __forceinline__ float ln_bound(float x)
+{
+  const float l = (float(__builtin_amdgcn_frexp_expf(x)) + __builtin_amdgcn_logf(__builtin_amdgcn_frexp_mantf(x))) * kLn2F;
+  return (x > 0.0f) ? l : -__builtin_inff();
+}
+
 // fresnel::complex<CONF, Spectrum> per channel (include/bbm/fresnel_complex.h:38-63); params = n RGB, k RGB
 struct FresnelComplexRGB
 {
@@ -261,22 +269,32 @@ struct He
     // compares consecutive terms, and near the series' peak they are nearly equal, so terms that differed by
     // an ulp would truncate the series one term early or late where D is tiny.
     double eg[3], cap[3];
+    float lng[3];
+    // non-Westin: eb (<= v_xy^2 tau^2 / 4) is the same small number on every channel, e^(-eb/64) bounds e^(-q_m')
+    // closely, and the cheap bound cap gm_m / m below is tested every 4th term instead
+    const double eb64 = (ADAPTIVE && !WESTIN && !converged) ? exp_dd(-double(eb[0]) * (1.0 / 64.0)) * (1.0 + 0x1p-10) : 0.0;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp_dd(-g[c]);
-    // Exact early exit (adaptive series only).  Past the peak (m + 1 >= g) every later term is at most
-    //   cap * gm_m / m,  cap = e^(-g) e^(-eb/64) (1 + 2^-10)
-    // (g^m'/m'! and 1/m' decrease, eb/m' >= eb/64 up to float rounding, the margin covers gm's per-step
-    // roundings).  Once that bound is below half an ulp of a channel's float sum (below 2^-150 while the sum is
-    // still 0) on all three channels, no later term can change any sum: the loop's only output is final, so
-    // it stops there with exactly the reference's result, wherever the reference's own stop (he.h:459) lies.
-    // Without it, lanes whose terms underflow to 0 (large eb: e^(-eb/m) for small m) never meet the stop
-    // rule (0 < 0 is false) and run all 64 terms -- one such lane in a wave keeps all 64 lanes busy.
-    if (ADAPTIVE)
+    for (int c = 0; c < 3; ++c)
     {
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        cap[c] = converged ? 0.0 : eg[c] * exp_dd(-double(eb[c]) * (1.0 / 64.0)) * (1.0 + 0x1p-10);
+      eg[c] = converged ? 0.0 : exp_dd(-g[c]);
+      lng[c] = (ADAPTIVE && WESTIN) ? ln_bound(float(g[c])) : 0.0f;
+      cap[c] = eg[c] * eb64;
     }
+    // Exact early exit (adaptive series only).  Past the peak (m + 1 >= g, r = g / (m + 1) <= 1) a later term
+    // m' in [m + 1, 64] is at most
+    //   e^(-g) (gm_m / m) e^(h(m')),   h(m') = -eb / m' + (m' - m) ln r
+    // (gm_m' <= gm_m r^(m' - m), 1/m' < 1/m, q_m' = float(eb / m') >= eb / m' up to float rounding).  h is concave
+    // in m', so its maximum over the range is at m* = sqrt(eb / -ln r) clamped to [m + 1, 64] -- a closed form.
+    // Once that bound (in the log domain, +0.01 for every rounding involved) is below half an ulp of a
+    // channel's float sum (2^-150 while the sum is 0) on all three channels, no later term can change any sum:
+    // the loop's only output is final, so it stops there with exactly the reference's result, wherever the
+    // reference's own stop (he.h:459) lies.  Without it, lanes whose terms underflow to 0 for small m (large eb)
+    // never meet the stop rule (0 < 0 is false) and run all 64 terms, and one such lane keeps its wave busy.
+    // Modelled on uniform hemisphere pairs (HeWestin defaults): wave-max 64 terms without the exit, 36 with the
+    // simpler bound e^(-g) e^(-eb/64) gm_m / m, 31.6 with this one tested every 8th term (31.1 every 4th, 30.8 with
+    // the exact tail maximum); measured HeWestin 1.36 -> 1.28 ms per 10 M pairs.  For the non-Westin series eb is
+    // small and the same on every channel, e^(-eb/64) is close, and that cheaper bound (every 4th term) stays:
+    // the concave one measured 0.89 -> 0.95 (every 8th) / 1.10 ms (every 4th) there.
 #ifdef BBM_HIP_HE_PROBE_NO_SERIES
     converged = true;       // timing probe only (tools/build_variant.sh): the prelude without the series
 #endif
@@ -304,16 +322,36 @@ struct He
       {
         converged = (fminf(fminf(term[0], term[1]), term[2]) < kEpsF) &&
                     (fminf(fminf(term[0], term[1]), term[2]) < fminf(fminf(last[0], last[1]), last[2]));
-        bool settled = (m & 3) == 0;      // tested every 4th term: the bound costs as much as a third of a term
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
+        if (!WESTIN && (m & 3) == 0)
         {
-          // half an ulp of sum[c] (2^-150 for 0 and subnormal sums)
-          const int e = (sum[c] > 0.0f) ? __builtin_amdgcn_frexp_expf(sum[c]) - 25 : -150;
-          const double half_ulp = __builtin_ldexp(1.0, max(e, -150));
-          settled = settled && (double(m) + 1.0 >= g[c]) && (cap[c] * double(gm[c]) * rm < half_ulp);
+          bool settled = true;
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+          {
+            const int e = (sum[c] > 0.0f) ? max(__builtin_amdgcn_frexp_expf(sum[c]) - 25, -150) : -150;
+            settled = settled && (double(m) + 1.0 >= g[c]) && (cap[c] * double(gm[c]) * rm < __builtin_ldexp(1.0, e));
+          }
+          converged = converged || settled;
         }
-        converged = converged || settled;
+        // Westin: the concave bound, tested every 8th term (a term ~100 VALU, the test ~70)
+        if (WESTIN && (m & 7) == 0)
+        {
+          bool settled = true;
+          const float ln_m = ln_bound(mf), ln_m1 = ln_bound(mf + 1.0f);
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+          {
+            const float lnr = lng[c] - ln_m1;                                // ln r <= 0 past the peak
+            float ms = (lnr < 0.0f) ? sqrtf(eb[c] / -lnr) : 64.0f;
+            ms = fminf(fmaxf(ms, mf + 1.0f), 64.0f);
+            const float h = -eb[c] / ms + (ms - mf) * lnr;
+            const float bound = ((-float(g[c]) + ln_bound(gm[c])) - ln_m) + h + 0.01f;
+            // ln of half an ulp of sum[c] (2^-150 for 0 and subnormal sums)
+            const int e = (sum[c] > 0.0f) ? max(__builtin_amdgcn_frexp_expf(sum[c]) - 25, -150) : -150;
+            settled = settled && (double(m) + 1.0 >= g[c]) && (bound < float(e) * kLn2F);
+          }
+          converged = converged || settled;
+        }
       }
     }
 #pragma unroll
