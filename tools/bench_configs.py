@@ -86,6 +86,27 @@ def _line(args, world, metric, value, unit, elapsed, config, extra):
     print(json.dumps(d), flush=True)
 
 
+GRAPH_REPS = 8
+
+
+def _graph(launch, reps):
+    """A CUDA(HIP) graph of `reps` calls of launch(stream), captured after one warm-up call (first-use host work
+    such as EPD's table build happens there, outside the capture)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        launch(side)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream()
+        for _ in range(reps):
+            launch(s)
+    torch.cuda.synchronize()
+    return g
+
+
 def bench_models(args, dist, rank, world):
     n = 10_000_000
     din = bbm_amd.fill_directions(SEED, 0, rank * n, n, mode=0)
@@ -95,18 +116,24 @@ def bench_models(args, dist, rank, world):
     per = {}
     total_t = 0.0
     names = _subset(args, [m for m in bbm_amd.model_names() if not m.startswith("Aggregate")])
+    reps = GRAPH_REPS
     for name in names:
         m = _merl_from(bbm_amd.CookTorrance()) if name == "Merl" else bbm_amd.BsdfModel(name)
-        elapsed, kern_ms = _timed(lambda: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=stream), args, dist, stream)
+        # one step = a HIP graph of `reps` back-to-back launches: a 10M-pair eval of the HBM-bound models takes
+        # ~35 us, less than one Python-side launch, so per-launch stepping would time the host, not the kernel
+        graph = _graph(lambda s: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=s), reps)
+        elapsed, step_ms = _timed(graph.replay, args, dist, stream)
+        kern_ms = step_ms / reps
         bpp = 20 if name in Z_ONLY else 36
         gbs = bpp * n / (kern_ms * 1e-3) / 1e9
-        per[name] = {"pairs_per_s": n * world * args.steps / elapsed, "kernel_ms": kern_ms, "GB_s": gbs,
+        per[name] = {"pairs_per_s": n * world * args.steps * reps / elapsed, "kernel_ms": kern_ms, "GB_s": gbs,
                      "roofline_frac": gbs / HBM_PEAK_GBS, "bytes_per_pair": bpp}
-        total_t += elapsed
+        total_t += elapsed / reps
     if rank == 0:
         _line(args, world, "BSDF evals/s (eval), all single bsdfmodels, 10M shared pairs per GPU (config 3)",
               len(names) * n * world * args.steps / total_t, "pairs/s", total_t / len(names),
-              {"workload": f"{len(names)} models x eval over {n} shared pairs per GPU, one kernel per model",
+              {"workload": f"{len(names)} models x eval over {n} shared pairs per GPU, one kernel per model "
+                           f"(replayed as a graph of {reps} launches per step)",
                "pairs_per_gpu": n, "parallelism": f"dp{world} (independent shards)"},
               {"scaling": "weak", "per_model": per})
 
