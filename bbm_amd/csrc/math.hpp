@@ -318,17 +318,49 @@ __device__ __forceinline__ void cossin_phi(v3 v, float& c, float& s)
 
 // backbone/native/include/backbone/math.h:115-126: Giles' single-precision erfinv polynomial.
 // For T = float the native backbone computes w = -log((1.0 - a)(1.0 + a)) in double and stores it
-// as float, then evaluates the Horner polynomial (util/poly.h:34-38) in double: the result is double.
-__device__ __forceinline__ double erfinv_d(float a)
+// as float, then evaluates the Horner polynomial (util/poly.h:34-38) in double: the result is double,
+// and its callers (ndf/beckmann.h:92-110) store it into a float.  erfinv_f returns that float with the
+// polynomial -- Giles' coefficients are floats, fitted for single precision -- evaluated by f32 FMAs:
+// within ~2 ulp of the double evaluation's rounding (the f32 w already differs by ~2 ulp) at a quarter of
+// the issue cycles (9 f32 FMAs against 18 f64 mul/add).  Sampled directions move by ~1e-7 relative.
+// w = float(-log((1 - a)(1 + a))): the reference's log is f64; here -log1p(-a^2) in f32 (a^2 as an exact
+// two-product, log1p by the u = 1 + x correction on the device logf, ~2 ulp) -- ~20 VALU instead of ~100 f64
+// instructions; the five erfinv calls of a Beckmann sample were its whole cost.
+__device__ __forceinline__ float erfinv_w(float a)
 {
-  // w = float(-log((1 - a)(1 + a))): the reference's log is f64; here -log1p(-a^2) in f32 (a^2 as an
-  // exact two-product, log1p by the u = 1 + x correction on the device logf, ~2 ulp) -- ~20 VALU
-  // instead of ~100 f64 instructions; the five erfinv calls of a Beckmann sample were its whole cost.
   const float a2 = a * a;
   const float a2e = __builtin_fmaf(a, a, -a2);          // a^2 = a2 + a2e exactly
   const float u = 1.0f - a2;                            // log1p(-a2 - a2e) = log1p(-a2) - a2e / (1 - a2)
   const float l1p = (u == 1.0f) ? -a2 : logf(u) * div_nr(-a2, u - 1.0f);
-  const float w = (u == 0.0f) ? __builtin_inff() : -(l1p - div_nr(a2e, u));   // a = +-1: -log(0) = inf
+  return (u == 0.0f) ? __builtin_inff() : -(l1p - div_nr(a2e, u));   // a = +-1: -log(0) = inf
+}
+__device__ __forceinline__ float erfinv_f(float a)
+{
+  const float w = erfinv_w(a);
+  float p;
+  if (w < 5)
+  {
+    const float x = w - 2.5f;
+    p = 2.81022636e-08f;
+    p = __builtin_fmaf(p, x, 3.43273939e-07f); p = __builtin_fmaf(p, x, -3.5233877e-06f);
+    p = __builtin_fmaf(p, x, -4.39150654e-06f); p = __builtin_fmaf(p, x, 0.00021858087f);
+    p = __builtin_fmaf(p, x, -0.00125372503f); p = __builtin_fmaf(p, x, -0.00417768164f);
+    p = __builtin_fmaf(p, x, 0.246640727f); p = __builtin_fmaf(p, x, 1.50140941f);
+  }
+  else
+  {
+    const float x = sqrtf(w) - 3.0f;
+    p = -0.000200214257f;
+    p = __builtin_fmaf(p, x, 0.000100950558f); p = __builtin_fmaf(p, x, 0.00134934322f);
+    p = __builtin_fmaf(p, x, -0.00367342844f); p = __builtin_fmaf(p, x, 0.00573950773f);
+    p = __builtin_fmaf(p, x, -0.0076224613f); p = __builtin_fmaf(p, x, 0.00943887047f);
+    p = __builtin_fmaf(p, x, 1.00167406f); p = __builtin_fmaf(p, x, 2.83297682f);
+  }
+  return p * a;
+}
+__device__ __forceinline__ double erfinv_d(float a)
+{
+  const float w = erfinv_w(a);
   if (w < 5)
   {
     const double x = w - 2.5;

@@ -15,6 +15,16 @@ namespace bbmhip {
 template<class NDF>
 __device__ __forceinline__ float vndf_pdf(const NDF& ndf, v3 view, v3 m, float D);
 
+// the sampler's erfinv, stored into a float (ndf/beckmann.h:99-106); -DBBM_HIP_ERFINV_D: the double evaluation (A/B)
+__device__ __forceinline__ float erfinv_s(float a)
+{
+#ifdef BBM_HIP_ERFINV_D
+  return float(erfinv_d(a));
+#else
+  return erfinv_f(a);
+#endif
+}
+
 // ndf::beckmann<CONF, Symmetry, Normalize> (include/ndf/beckmann.h:40-213)
 template<bool Aniso, bool Normalize>
 struct Beckmann
@@ -59,13 +69,13 @@ struct Beckmann
     xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_dn(-(vs.z * vs.z))));
     for (int i = 0; i < 3; ++i)
     {
-      const float slope = float(erfinv_d(x));
+      const float slope = erfinv_s(x);
       const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_dn(-slope * slope) - xc0);
       const float der = float(1.0 - slope * tanT);
       x -= div_nr(val, der);
     }
     float s0 = 0.0f, s1 = 0.0f;
-    if (x > -1.0 && x < +1.0) { s0 = float(erfinv_d(x)); s1 = float(erfinv_d(float(2.0 * xc1 - 1.0))); }
+    if (x > -1.0 && x < +1.0) { s0 = erfinv_s(x); s1 = erfinv_s(float(2.0 * xc1 - 1.0)); }
     float c, s;
     cossin_phi(vs, c, s);
     const float u0 = ((0.0f + c * s0) + -s * s1) * au;
