@@ -48,6 +48,10 @@ namespace bbm {
     //! \brief SoA view of N writable 3-vectors / RGB spectra in device memory
     struct soa3_out { float* x; float* y; float* z; };
 
+    //! \brief The same views over f64 arrays: the doubleRGB configuration (Value = double)
+    struct soa3d { const double* x; const double* y; const double* z; };
+    struct soa3d_out { double* x; double* y; double* z; };
+
     //! \brief Error raised when the HIP backbone rejects a call
     struct error : public std::runtime_error
     {
@@ -127,7 +131,8 @@ namespace bbm {
       {
         using C = get_config<MODEL>;
         using M = std::decay_t<MODEL>;
-        static_assert(std::is_same_v<Value_t<C>, float>, "the HIP backbone evaluates floatRGB-style configs (Value = float)");
+        static_assert(std::is_same_v<Value_t<C>, float> || std::is_same_v<Value_t<C>, double>,
+                      "the HIP backbone evaluates floatRGB- and doubleRGB-style configs (Value = float / double)");
 #ifdef _BBM_LAMBERTIAN_H_
         if constexpr (std::is_same_v<M, bbm::lambertian<C>>) return "Lambertian";
         else
@@ -297,6 +302,15 @@ namespace bbm {
       return p;
     }
 
+    //! \brief The same vector in double (doubleRGB models: the attributes unrounded)
+    template<typename MODEL>
+      inline std::vector<double> parameters_f64(const MODEL& model)
+    {
+      std::vector<double> p;
+      for(auto& v : bbm::parameter_values(model, bsdf_attr(0x1F))) p.push_back(double(v));
+      return p;
+    }
+
 #ifdef _BBM_MERL_H_
     namespace detail {
       //! \brief device float4 table of a MERL file (bbm_hip_merl_table), built once per file and kept for the
@@ -390,6 +404,8 @@ namespace bbm {
       inline model_desc describe(const MODEL& model)
     {
       using M = std::decay_t<MODEL>;
+      static_assert(std::is_same_v<Value_t<get_config<M>>, float>,
+                    "float32 entry points take floatRGB-style models; doubleRGB models use the soa3d overloads");
 #ifdef _BBM_MERL_H_
       // Merl: ndf_sampler<merl_data<C, "Merl">, 90, 1> (staticmodel/merl.h:224-225), identified by its file
       // (toString, merl.h:161-164); a bare merl_data (placeholder sampler, merl.h:108-115) is rejected
@@ -549,6 +565,33 @@ namespace bbm {
                               bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                               const uint8_t* mask=nullptr, void* stream=nullptr)
     { reflectance(describe(model), out, n, rgb, component, unit, mask, stream); }
+
+    //! \brief doubleRGB (Value = double) models on f64 SoA arrays: eval + pdf, evaluated in f64 on the device
+    //! (bbm_hip_eval_pdf_f64).  MODEL must have a single kernel (single model or fused aggregate) with doubleRGB
+    //! kernels (bbm_hip_model_has_f64: Lambertian, OrenNayar, the microfacet compositions and their
+    //! Aggregate(Lambertian, X) fits); any other model is rejected with BBM_HIP_ERR_UNSUPPORTED.
+    template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
+      inline void eval_pdf(const MODEL& model, soa3d in, soa3d out, size_t n, soa3d_out rgb, double* p,
+                           bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                           const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      static const int id = id_of(detail::single_name<MODEL>());
+      const std::vector<double> prm = parameters_f64(model);
+      check(bbm_hip_eval_pdf_f64(id, prm.data(), int(prm.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+                                 uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, p, stream));
+    }
+
+    //! \brief doubleRGB reflectance of N out directions (bbm_hip_reflectance_f64)
+    template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
+      inline void reflectance(const MODEL& model, soa3d out, size_t n, soa3d_out rgb,
+                              bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                              const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      static const int id = id_of(detail::single_name<MODEL>());
+      const std::vector<double> prm = parameters_f64(model);
+      check(bbm_hip_reflectance_f64(id, prm.data(), int(prm.size()), out.x, out.y, out.z, mask, n, uint32_t(component),
+                                    uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+    }
 
     //! \brief Sample losses of include/loss/*.h, for loss_sums
     enum class loss_t : int { nganL2 = BBM_LOSS_NGAN_L2, lowL2 = BBM_LOSS_LOW_L2, bieronL2 = BBM_LOSS_BIERON_L2,

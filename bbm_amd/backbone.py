@@ -49,9 +49,18 @@ def _torch():
     return torch
 
 
-def _soa(t, n=None, what="direction"):
-    """Return (x_ptr, y_ptr, z_ptr, n) for a (3, N) tensor or a tuple of three 1-D tensors."""
+def _is_f64(t):
+    """True if the direction rows are float64 (the doubleRGB configuration)."""
     torch = _torch()
+    rows = list(t) if isinstance(t, (tuple, list)) else [t]
+    return bool(rows) and isinstance(rows[0], torch.Tensor) and rows[0].dtype == torch.float64
+
+
+def _soa(t, n=None, what="direction", dtype=None):
+    """Return (x_ptr, y_ptr, z_ptr, n) for a (3, N) tensor or a tuple of three 1-D tensors of `dtype`
+    (float32 unless given)."""
+    torch = _torch()
+    dtype = torch.float32 if dtype is None else dtype
     if isinstance(t, (tuple, list)):
         rows = list(t)
     else:
@@ -59,8 +68,8 @@ def _soa(t, n=None, what="direction"):
             raise ValueError(f"{what}: expected a (3, N) tensor, got {tuple(t.shape)}")
         rows = [t[0], t[1], t[2]]
     for r in rows:
-        if not isinstance(r, torch.Tensor) or r.dtype != torch.float32 or not r.is_cuda:
-            raise TypeError(f"{what}: expected float32 CUDA tensors")
+        if not isinstance(r, torch.Tensor) or r.dtype != dtype or not r.is_cuda:
+            raise TypeError(f"{what}: expected {str(dtype).replace('torch.', '')} CUDA tensors")
         if r.dim() != 1 or r.stride(0) != 1:
             raise ValueError(f"{what}: rows must be contiguous 1-D tensors")
     m = rows[0].numel()
@@ -83,12 +92,13 @@ def _mask_ptr(mask, n):
     return mask.data_ptr(), mask
 
 
-def _out_rows(t, rows, n, device, what):
-    """Validate a caller-supplied output buffer before its row pointers reach a kernel: float32, on the
-    inputs' device, shape (rows, n) (or (n,) for rows == 0) with every row contiguous."""
+def _out_rows(t, rows, n, device, what, dtype=None):
+    """Validate a caller-supplied output buffer before its row pointers reach a kernel: float32 (or `dtype`), on
+    the inputs' device, shape (rows, n) (or (n,) for rows == 0) with every row contiguous."""
     torch = _torch()
-    if not isinstance(t, torch.Tensor) or t.dtype != torch.float32:
-        raise TypeError(f"{what}: expected a float32 CUDA tensor")
+    dtype = torch.float32 if dtype is None else dtype
+    if not isinstance(t, torch.Tensor) or t.dtype != dtype:
+        raise TypeError(f"{what}: expected a {str(dtype).replace('torch.', '')} CUDA tensor")
     if not t.is_cuda or t.device != device:
         raise ValueError(f"{what}: must live on {device}, got {t.device}")
     shape = (n,) if rows == 0 else (rows, n)
@@ -255,9 +265,43 @@ class BsdfModel:
     def _pptr(self):
         return self._params.ctypes.data_as(ctypes.c_void_p)
 
-    def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
-                 rgb=None, pdf=None, stream=None, mode=3):
+    def has_f64(self):
+        """True if the model has doubleRGB kernels (bbm_hip_model_has_f64)."""
+        return _lib.check(_lib.load().bbm_hip_model_has_f64(self.model_id)) == 1
+
+    def _params_f64(self, params64):
+        if params64 is None:
+            return np.ascontiguousarray(self._params, dtype=np.float64)
+        v = np.ascontiguousarray(params64, dtype=np.float64).reshape(-1)
+        if v.size != self._params.size:
+            raise ValueError(f"{self.name}: expected {self._params.size} parameters, got {v.size}")
+        return v
+
+    def _eval_pdf_f64(self, in_, out, component, unit, mask, rgb, pdf, stream, params64):
+        """doubleRGB (Value = double): float64 directions -> float64 eval RGB and pdf (bbm_hip_eval_pdf_f64).
+        Parameters: params64 if given, else the model's (float) parameter vector widened to double."""
         torch = _torch()
+        f64 = torch.float64
+        ix, iy, iz, n = _soa(in_, what="in", dtype=f64)
+        ox, oy, oz, _ = _soa(out, n, what="out", dtype=f64)
+        mptr, _keep = _mask_ptr(mask, n)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rgb = torch.empty((3, n), dtype=f64, device=dev) if rgb is None else _out_rows(rgb, 3, n, dev, "rgb", f64)
+        pdf = torch.empty((n,), dtype=f64, device=dev) if pdf is None else _out_rows(pdf, 0, n, dev, "pdf", f64)
+        p = self._params_f64(params64)
+        _on_stream(stream, _keep, rgb, pdf)
+        _lib.check(_lib.load().bbm_hip_eval_pdf_f64(
+            self.model_id, p.ctypes.data_as(ctypes.c_void_p), p.size, ix, iy, iz, ox, oy, oz, mptr, n, int(component),
+            int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(), rgb[2].data_ptr(), pdf.data_ptr(), _stream_ptr(stream)))
+        return rgb, pdf
+
+    def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
+                 rgb=None, pdf=None, stream=None, mode=3, params64=None):
+        torch = _torch()
+        if _is_f64(in_):
+            rgb, pdf = self._eval_pdf_f64(in_, out, component, unit, mask, rgb if mode & 1 else None,
+                                          pdf if mode & 2 else None, stream, params64)
+            return (rgb if mode & 1 else None), (pdf if mode & 2 else None)
         ix, iy, iz, n = _soa(in_, what="in")
         ox, oy, oz, _ = _soa(out, n, what="out")
         mptr, _keep = _mask_ptr(mask, n)
@@ -318,9 +362,22 @@ class BsdfModel:
                                       _stream_ptr(stream)))
         return BsdfSample(d, p, f)
 
-    def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
-        """Spectrum reflectance(out, component, unit, mask) for N directions -> (3, N) RGB."""
+    def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None,
+                    params64=None):
+        """Spectrum reflectance(out, component, unit, mask) for N directions -> (3, N) RGB (float64 directions:
+        the doubleRGB kernels, float64 RGB)."""
         torch = _torch()
+        if _is_f64(out):
+            ox, oy, oz, n = _soa(out, what="out", dtype=torch.float64)
+            mptr, _keep = _mask_ptr(mask, n)
+            dev = (out[0] if isinstance(out, (tuple, list)) else out).device
+            rgb = torch.empty((3, n), dtype=torch.float64, device=dev)
+            p = self._params_f64(params64)
+            _on_stream(stream, _keep, rgb)
+            _lib.check(_lib.load().bbm_hip_reflectance_f64(
+                self.model_id, p.ctypes.data_as(ctypes.c_void_p), p.size, ox, oy, oz, mptr, n, int(component),
+                int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
+            return rgb
         ox, oy, oz, n = _soa(out, what="out")
         mptr, _keep = _mask_ptr(mask, n)
         dev = (out[0] if isinstance(out, (tuple, list)) else out).device

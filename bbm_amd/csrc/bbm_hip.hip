@@ -13,6 +13,7 @@
 #include "../../include/bbm_hip.h"
 #include "kernels.hpp"
 #include "models.hpp"
+#include "f64.hpp"
 
 namespace bbmhip {
 
@@ -608,6 +609,75 @@ int bbm_hip_reflectance(int model_id, const float* params, int nparams,
   a.ox = out_x; a.oy = out_y; a.oz = out_z; a.mask = mask; a.r = r; a.g = g; a.b = b;
   a.component = component & kFlagAll;
   return e->reflectance(a, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------------------- doubleRGB (f64.hip)
+
+static int prepare_f64(int model_id, const double* params, int nparams, const ModelEntry*& e,
+                       const f64::F64Launchers*& l, f64::ParamBlockF64& p)
+{
+  e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  l = f64::f64_launchers(e->name);
+  if (!l) return fail(BBM_HIP_ERR_UNSUPPORTED, std::string(e->name) + ": no doubleRGB kernel");
+  if (nparams != e->nparams)
+    return fail(BBM_HIP_ERR_INVALID_ARG, std::string(e->name) + ": expected " + std::to_string(e->nparams) +
+                                             " parameters, got " + std::to_string(nparams));
+  if (nparams > 0 && !params) return fail(BBM_HIP_ERR_INVALID_ARG, "params is NULL");
+  std::memset(&p, 0, sizeof(p));
+  for (int i = 0; i < nparams; ++i) p.v[i] = params[i];
+  return BBM_HIP_OK;
+}
+
+int bbm_hip_model_has_f64(int model_id)
+{
+  const ModelEntry* e = entry(model_id);
+  if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
+  return f64::f64_launchers(e->name) ? 1 : 0;
+}
+
+int bbm_hip_eval_pdf_f64(int model_id, const double* params, int nparams,
+                         const double* in_x, const double* in_y, const double* in_z,
+                         const double* out_x, const double* out_y, const double* out_z,
+                         const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                         double* r, double* g, double* b, double* pdf, void* stream)
+{
+  (void)unit;
+  const ModelEntry* e;
+  const f64::F64Launchers* l;
+  f64::EvalArgsF64 a;
+  std::memset(&a, 0, sizeof(a));
+  int rc = prepare_f64(model_id, params, nparams, e, l, a.p);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if (!in_x || !in_y || !in_z || !out_x || !out_y || !out_z) return fail(BBM_HIP_ERR_INVALID_ARG, "direction pointer is NULL");
+  if (!r || !g || !b || !pdf) return fail(BBM_HIP_ERR_INVALID_ARG, "output pointer is NULL");
+  a.ix = in_x; a.iy = in_y; a.iz = in_z; a.ox = out_x; a.oy = out_y; a.oz = out_z;
+  a.mask = mask; a.r = r; a.g = g; a.b = b; a.pdf = pdf;
+  a.n = n;
+  a.component = component & kFlagAll;
+  return l->eval_pdf(a, static_cast<hipStream_t>(stream));
+}
+
+int bbm_hip_reflectance_f64(int model_id, const double* params, int nparams,
+                            const double* out_x, const double* out_y, const double* out_z,
+                            const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                            double* r, double* g, double* b, void* stream)
+{
+  (void)unit;
+  const ModelEntry* e;
+  const f64::F64Launchers* l;
+  f64::ReflArgsF64 a;
+  std::memset(&a, 0, sizeof(a));
+  int rc = prepare_f64(model_id, params, nparams, e, l, a.p);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if (!out_x || !out_y || !out_z) return fail(BBM_HIP_ERR_INVALID_ARG, "out direction pointer is NULL");
+  if (!r || !g || !b) return fail(BBM_HIP_ERR_INVALID_ARG, "reflectance output pointer is NULL");
+  a.ox = out_x; a.oy = out_y; a.oz = out_z; a.mask = mask; a.r = r; a.g = g; a.b = b;
+  a.n = n;
+  a.component = component & kFlagAll;
+  return l->reflectance(a, static_cast<hipStream_t>(stream));
 }
 
 int bbm_hip_model_param_attrs(int model_id, uint32_t* out, int capacity)

@@ -1,0 +1,161 @@
+// bbm_amd/csrc/f64.hip -- doubleRGB kernels (f64.hpp) and their registry by model name.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <string>
+
+#include "../../include/bbm_hip.h"
+#include "f64.hpp"
+
+namespace bbmhip {
+
+int fail(int code, const std::string& msg);
+
+namespace f64 {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint64_t kMaxBlocks = 1u << 20;
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+// V pairs per thread-iteration: V = 2 loads / stores 16 B per array (every pointer 16 B aligned, checked on the
+// host), V = 1 is the fallback for 8 B-aligned arrays.  A wave touches 64 x 8V contiguous bytes per array.
+template<int V>
+__device__ __forceinline__ void ld(const double* p, uint64_t t, double* v)
+{
+  if (V == 2)
+  {
+    const dv2 x = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p) + t);
+    v[0] = x.x; v[1] = x.y;
+  }
+  else v[0] = __builtin_nontemporal_load(p + t);
+}
+template<int V>
+__device__ __forceinline__ void st(double* p, uint64_t t, const double* v)
+{
+  if (V == 2) __builtin_nontemporal_store(dv2{v[0], v[1]}, reinterpret_cast<dv2*>(p) + t);
+  else __builtin_nontemporal_store(v[0], p + t);
+}
+
+template<class Model, int V, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_eval_pdf_f64(EvalArgsF64 a)
+{
+  const Model m(a.p.v);
+  const uint64_t nv = a.n / V;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < nv; t += stride)
+  {
+    double ix[V], iy[V], iz[V], ox[V], oy[V], oz[V], r[V], g[V], b[V], p[V];
+    ld<V>(a.ix, t, ix); ld<V>(a.iy, t, iy); ld<V>(a.iz, t, iz);
+    ld<V>(a.ox, t, ox); ld<V>(a.oy, t, oy); ld<V>(a.oz, t, oz);
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+    {
+      const uint32_t comp = (!MASK || a.mask[t * V + j]) ? a.component : 0u;
+      double rgb[3];
+      m.eval_pdf(mk(ix[j], iy[j], iz[j]), mk(ox[j], oy[j], oz[j]), comp, rgb, p[j]);
+      r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
+    }
+    st<V>(a.r, t, r); st<V>(a.g, t, g); st<V>(a.b, t, b); st<V>(a.pdf, t, p);
+  }
+  if (V == 2 && blockIdx.x == 0 && threadIdx.x == 0 && (a.n & 1))
+  {
+    const uint64_t i = a.n - 1;
+    const uint32_t comp = (!MASK || a.mask[i]) ? a.component : 0u;
+    double rgb[3], p;
+    m.eval_pdf(mk(a.ix[i], a.iy[i], a.iz[i]), mk(a.ox[i], a.oy[i], a.oz[i]), comp, rgb, p);
+    a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2]; a.pdf[i] = p;
+  }
+}
+
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_reflectance_f64(ReflArgsF64 a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+  {
+    double rgb[3];
+    m.reflectance(mk(a.ox[i], a.oy[i], a.oz[i]), (!MASK || a.mask[i]) ? a.component : 0u, rgb);
+    a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2];
+  }
+}
+
+unsigned grid(uint64_t units)
+{
+  const uint64_t b = (units + kBlock - 1) / kBlock;
+  return unsigned(b < 1 ? 1 : (b > kMaxBlocks ? kMaxBlocks : b));
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int launched(const char* what)
+{
+  const hipError_t e = hipGetLastError();
+  return (e == hipSuccess) ? 0 : fail(BBM_HIP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template<class Model>
+int launch_eval_pdf(const EvalArgsF64& a, hipStream_t s)
+{
+  const bool v2 = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
+                  aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
+  const unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
+  if (v2 && a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (v2) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+  return launched("k_eval_pdf_f64");
+}
+
+template<class Model>
+int launch_reflectance(const ReflArgsF64& a, hipStream_t s)
+{
+  if (a.mask) hipLaunchKernelGGL((k_reflectance_f64<Model, true>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_reflectance_f64<Model, false>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
+  return launched("k_reflectance_f64");
+}
+
+struct Entry { const char* name; F64Launchers l; };
+#define BBM_HIP_F64(NAME, M) {NAME, {&launch_eval_pdf<M>, &launch_reflectance<M>}}
+// names as in the floatRGB registry (bbm_hip.hip); aliases share a composition as they do there
+const Entry kF64[] = {
+  BBM_HIP_F64("Lambertian", Lambertian),
+  BBM_HIP_F64("OrenNayar", OrenNayar),
+  BBM_HIP_F64("CookTorrance", CookTorranceM),
+  BBM_HIP_F64("LowCookTorrance", CookTorranceM),   // bsdfmodel/low.h:32-33
+  BBM_HIP_F64("GGX", GGXM),
+  BBM_HIP_F64("CookTorranceWalter", CookTorranceWalterM),
+  BBM_HIP_F64("CookTorranceHeitz", CookTorranceHeitzM),
+  BBM_HIP_F64("GGXHeitz", GGXHeitzM),
+  BBM_HIP_F64("NganCookTorrance", NganCookTorranceM),
+  BBM_HIP_F64("PhongWalter", PhongWalterM),
+  BBM_HIP_F64("Ribardiere", RibardiereM),
+  BBM_HIP_F64("RibardiereAnisotropic", RibardiereAnisoM),
+  BBM_HIP_F64("LowMicrofacet", LowMicrofacetM),
+  BBM_HIP_F64("LowMicrofacetFit", LowMicrofacetM),
+  BBM_HIP_F64("Aggregate<Lambertian,CookTorrance>", AggCookTorranceM),
+  BBM_HIP_F64("Aggregate<Lambertian,LowCookTorrance>", AggCookTorranceM),
+  BBM_HIP_F64("Aggregate<Lambertian,GGX>", AggGGXM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganCookTorrance>", AggNganCookTorranceM),
+  BBM_HIP_F64("Aggregate<Lambertian,LowMicrofacetFit>", AggLowMicrofacetM),
+};
+#undef BBM_HIP_F64
+
+static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
+              CookTorranceHeitzM::kParams == 6 && GGXHeitzM::kParams == 6 && NganCookTorranceM::kParams == 5 &&
+              PhongWalterM::kParams == 5 && RibardiereM::kParams == 6 && RibardiereAnisoM::kParams == 7 &&
+              LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8, "f64 nparams must match the floatRGB registry");
+
+}  // namespace
+
+const F64Launchers* f64_launchers(const char* name)
+{
+  if (!name) return nullptr;
+  for (const auto& e : kF64)
+    if (std::strcmp(e.name, name) == 0) return &e.l;
+  return nullptr;
+}
+
+}  // namespace f64
+}  // namespace bbmhip

@@ -2,7 +2,7 @@
 """bench.py -- BASELINE.json metric: CookTorrance eval+pdf pairs/s, 100M pairs per GPU, f32.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong] [--pairs P] [--model NAME]
-                    [--no-cpu] [--workload evalpdf|models|sample|fit|selftest]
+                    [--no-cpu] [--workload evalpdf|models|sample|fit|f64|selftest]
 
 One step = one fused eval+pdf pass (bbm_hip_eval_pdf) of the model over the GPU's shard of synthetic
 direction pairs already resident in HBM (SoA f32, generated on the device by the counter-based
@@ -67,10 +67,11 @@ def parse(argv=None):
                                                    "(counter passes profile one model at a time)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "selftest"],
+    ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "f64", "selftest"],
                     help="evalpdf: the BASELINE metric (config 2, default); models: every model's eval over shared "
                          "pairs (config 3); sample: importance-sample -> eval -> pdf MC loop (config 4); fit: "
-                         "multi-probe fitting loss of a compass step over the MERL grid (config 5); selftest: the "
+                         "multi-probe fitting loss of a compass step over the MERL grid (config 5); f64: the doubleRGB "
+                         "path (--model over --pairs f64 pairs + every doubleRGB model); selftest: the "
                          "multi-rank harness on the CPU (gloo), no GPU")
     return ap.parse_args(argv)
 

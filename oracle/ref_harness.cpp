@@ -152,6 +152,15 @@ int bbmref_reflectance(const char* name, const float* p, int np, size_t n,
   return 0;
 }
 
+int bbmref_reflectance_double(const char* name, const float* p, int np, size_t n,
+                              const float* ox, const float* oy, const float* oz,
+                              uint32_t component, uint32_t unit, double* r, double* g, double* b)
+{
+  auto e = find(name); if(!e || !e->reflectance_d) return -1;
+  e->reflectance_d(p, np, n, ox, oy, oz, component, unit, r, g, b);
+  return 0;
+}
+
 // bbm::fromString of the model `name` (a model string as printed by toString / stored in fits/*.fit) -> its
 // parameter vector (All | Dependent, declaration order); <0 if the reference rejects the string
 int bbmref_from_string(const char* name, const char* str, float* out, int cap)

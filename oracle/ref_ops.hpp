@@ -183,15 +183,16 @@ struct ops
     }
   }
 
+  template<typename OUT>
   static void reflectance(const float* p, int np, size_t n, const float* ox, const float* oy, const float* oz,
-                          uint32_t component, uint32_t unit, float* r, float* g, float* b)
+                          uint32_t component, uint32_t unit, OUT* r, OUT* g, OUT* b)
   {
     const M m = make(p, np);
     for(size_t i = 0; i < n; ++i)
     {
       Vec3d out(Value(ox[i]), Value(oy[i]), Value(oz[i]));
       auto e = m.reflectance(out, bbm::bsdf_flag(component), bbm::unit_t(unit));
-      r[i] = float(e[0]); g[i] = float(e[1]); b[i] = float(e[2]);
+      r[i] = OUT(e[0]); g[i] = OUT(e[1]); b[i] = OUT(e[2]);
     }
   }
 };
@@ -207,6 +208,7 @@ struct entry
   void (*sample_f)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*, float*, uint32_t*, int);
   void (*reflectance_f)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*);
   int (*from_string)(const char*, float*, int) = nullptr;
+  void (*reflectance_d)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, double*, double*, double*) = nullptr;
 };
 
 #define BBMREF_ENTRY(MODEL) BBMREF_ENTRY_NS(bbm, MODEL)
@@ -218,8 +220,9 @@ struct entry
          &ops<NS::MODEL<bbm::floatRGB>>::template evalpdf<float>, \
          &ops<NS::MODEL<bbm::doubleRGB>>::template evalpdf<double>, \
          &ops<NS::MODEL<bbm::floatRGB>>::template sample<float>, \
-         &ops<NS::MODEL<bbm::floatRGB>>::reflectance, \
-         &ops<NS::MODEL<bbm::floatRGB>>::from_string }
+         &ops<NS::MODEL<bbm::floatRGB>>::template reflectance<float>, \
+         &ops<NS::MODEL<bbm::floatRGB>>::from_string, \
+         &ops<NS::MODEL<bbm::doubleRGB>>::template reflectance<double> }
 
 
 } // namespace bbmref

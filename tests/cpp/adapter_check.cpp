@@ -467,6 +467,56 @@ static bool check_loss(const MODEL& fitted, const MODEL& reference, size_t n, un
   return ok;
 }
 
+// doubleRGB through the adapter's soa3d overloads (bbm_hip_eval_pdf_f64 / bbm_hip_reflectance_f64) vs the same
+// model object evaluated per pair by the reference (Value = double): random double directions (in on the upper
+// hemisphere, out on the sphere), eval + pdf + reflectance, the 1e-5 bar per lane and the worst relative error
+template<typename MODEL>
+static bool check_model_f64(const MODEL& model, size_t n, unsigned seed)
+{
+  using Vec3d = typename MODEL::Vec3d;
+  std::mt19937_64 rng(seed);
+  std::uniform_real_distribution<double> u(0.0, 1.0);
+  std::vector<double> h[6];
+  for(auto& v : h) v.resize(n);
+  for(size_t i = 0; i < n; ++i)
+    for(int k = 0; k < 2; ++k)
+    {
+      const double z = k == 0 ? u(rng) : 2.0 * u(rng) - 1.0, phi = 6.283185307179586 * u(rng);
+      const double s = std::sqrt(std::max(1.0 - z * z, 0.0));
+      h[3 * k + 0][i] = s * std::cos(phi); h[3 * k + 1][i] = s * std::sin(phi); h[3 * k + 2][i] = z;
+    }
+  std::vector<double*> d(13, nullptr);   // in xyz, out xyz, eval rgb, pdf, reflectance rgb
+  for(auto& p : d) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(double)));
+  for(int k = 0; k < 6; ++k) HIPCHECK(hipMemcpy(d[size_t(k)], h[k].data(), n * sizeof(double), hipMemcpyHostToDevice));
+  bbm::hip::eval_pdf(model, bbm::hip::soa3d{d[0], d[1], d[2]}, bbm::hip::soa3d{d[3], d[4], d[5]}, n,
+                     bbm::hip::soa3d_out{d[6], d[7], d[8]}, d[9]);
+  bbm::hip::reflectance(model, bbm::hip::soa3d{d[3], d[4], d[5]}, n, bbm::hip::soa3d_out{d[10], d[11], d[12]});
+  std::vector<double> g[4], rf[3];
+  for(int k = 0; k < 4; ++k) { g[k].resize(n); HIPCHECK(hipMemcpy(g[k].data(), d[size_t(6 + k)], n * sizeof(double), hipMemcpyDeviceToHost)); }
+  for(int k = 0; k < 3; ++k) { rf[k].resize(n); HIPCHECK(hipMemcpy(rf[k].data(), d[size_t(10 + k)], n * sizeof(double), hipMemcpyDeviceToHost)); }
+  for(auto& p : d) (void)hipFree(p);
+  size_t bad = 0;
+  double worst = 0;
+  auto lane = [&](double got, double want) {
+    const bool ok = got == want || (std::isnan(got) && std::isnan(want)) ||
+                    std::fabs(got - want) <= 1e-5 * std::max(std::fabs(want), std::numeric_limits<double>::min());
+    if(!ok) ++bad;
+    if(std::fabs(want) >= std::numeric_limits<double>::min()) worst = std::max(worst, relerr(got, want));
+  };
+  for(size_t i = 0; i < n; ++i)
+  {
+    const Vec3d vin(h[0][i], h[1][i], h[2][i]), vout(h[3][i], h[4][i], h[5][i]);
+    const auto e = model.eval(vin, vout);
+    const auto r = model.reflectance(vout);
+    for(int c = 0; c < 3; ++c) { lane(g[c][i], double(e[c])); lane(rf[c][i], double(r[c])); }
+    lane(g[3][i], double(model.pdf(vin, vout)));
+  }
+  const bool ok = bad == 0 && worst <= 1e-10;
+  std::printf("{\"model\": \"%s\", \"config\": \"doubleRGB\", \"n\": %zu, \"violations\": %zu, \"max_rel_normal\": %.3e, \"ok\": %s}\n",
+              json_escape(label(model)).c_str(), n, bad, worst, ok ? "true" : "false");
+  return ok;
+}
+
 // a synthetic MERL-MIT .binary (three uint32 dimensions, then R, G, B planes of doubles): smooth in theta_h,
 // theta_d and phi_d, positive, distinct per channel
 static std::string write_merl(const std::string& path)
@@ -548,6 +598,23 @@ int main()
     auto q = bbm::parameter_values(br, bbm::bsdf_attr(0x1F));
     for(auto& x : q) x = float(x) * 0.9f;
     ok &= check_loss(bf, br, 1 << 16, seed++);
+  }
+  // doubleRGB (Value = double): every model with f64 kernels, by type, and two published-fit aggregates
+  using D = bbm::doubleRGB;
+#define CHECK_D(...) ok &= check_model_f64(__VA_ARGS__(), n, seed++);
+  CHECK_D(bbm::lambertian<D>) CHECK_D(bbm::orennayar<D>) CHECK_D(bbm::cooktorrance<D>) CHECK_D(bbm::lowcooktorrance<D>)
+  CHECK_D(bbm::ggx<D>) CHECK_D(bbm::cooktorrancewalter<D>) CHECK_D(bbm::cooktorranceheitz<D>) CHECK_D(bbm::ggxheitz<D>)
+  CHECK_D(bbm::ngancooktorrance<D>) CHECK_D(bbm::phongwalter<D>) CHECK_D(bbm::ribardiere<D>)
+  CHECK_D(bbm::ribardiereanisotropic<D>) CHECK_D(bbm::lowmicrofacet<D>) CHECK_D(bbm::lowmicrofacetfit<D>)
+  CHECK_D(bbm::aggregatemodel<bbm::lambertian<D>, bbm::cooktorrance<D>>)
+  CHECK_D(bbm::aggregatemodel<bbm::lambertian<D>, bbm::ngancooktorrance<D>>)
+#undef CHECK_D
+  {
+    // attributes that are not floats reach the kernel unrounded
+    bbm::cooktorrance<D> ct_d;
+    auto p = bbm::parameter_values(ct_d);
+    p[3] = 0.1 + 1e-12; p[4] = 1.5 + 3e-12;
+    ok &= check_model_f64(ct_d, n, seed++);
   }
   return ok ? 0 : 1;
 }

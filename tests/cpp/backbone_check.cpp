@@ -69,7 +69,7 @@
 namespace config_check {
   BBM_CHECK_CONFIG(bbm::floatRGB);
   BBM_CHECK_CONFIG(bbm::doubleRGB);
-  static_assert(bbm::floatRGB::device_batch && !bbm::doubleRGB::device_batch);
+  static_assert(bbm::floatRGB::device_batch && bbm::doubleRGB::device_batch);
   static_assert(std::is_same_v<bbm::get_config<bbm::cooktorrance<bbm::floatRGB>>, bbm::floatRGB>);
 }
 
@@ -196,6 +196,17 @@ int main()
     const auto c = bbm::hip::describe(bbm::aggregatemodel<bbm::cooktorrance<F>, bbm::ggx<F>>());
     if(d.composed() || std::string(bbm_hip_model_name(d.ids[0])) != "Aggregate<Lambertian,NganHe>" || !c.composed()) ++failures;
   }
+
+  // 4. doubleRGB: the models with f64 kernels (bbm_hip_*_f64) resolve by type to a registry entry that has them
+  using D = bbm::doubleRGB;
+#define F64(...) { const int id = bbm::hip::id_of(bbm::hip::detail::single_name<__VA_ARGS__>()); \
+                   if(bbm_hip_model_has_f64(id) != 1) { std::printf("{\"f64_missing\": \"%s\"}\n", #__VA_ARGS__); ++failures; } }
+  F64(bbm::lambertian<D>) F64(bbm::orennayar<D>) F64(bbm::cooktorrance<D>) F64(bbm::lowcooktorrance<D>) F64(bbm::ggx<D>)
+  F64(bbm::cooktorrancewalter<D>) F64(bbm::cooktorranceheitz<D>) F64(bbm::ggxheitz<D>) F64(bbm::ngancooktorrance<D>)
+  F64(bbm::phongwalter<D>) F64(bbm::ribardiere<D>) F64(bbm::ribardiereanisotropic<D>) F64(bbm::lowmicrofacet<D>)
+  F64(bbm::lowmicrofacetfit<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::cooktorrance<D>>)
+  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::ggx<D>>)
+#undef F64
 
   // an unknown model string fails loudly with the library's error
   try { (void)bbm::hip::from_string("NoSuchModel(albedo = 1)"); ++failures; }

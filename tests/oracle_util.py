@@ -115,6 +115,39 @@ def ref_reflectance(name, params, dout, component=3, unit=0):
     return res
 
 
+def ref_eval_pdf_double(name, params, din, dout, component=3, unit=0, nthreads=1):
+    """(4, N) float64: eval RGB + pdf from the reference's doubleRGB configuration (float parameters and directions
+    widened to double, as the GPU's f64 path receives them)."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    din = np.ascontiguousarray(din, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n = din.shape[1]
+    res = np.zeros((4, n), np.float64)
+    rc = lib.bbmref_eval_pdf_double(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(din[0]),
+                                    _fp(din[1]), _fp(din[2]), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]),
+                                    ctypes.c_uint32(component), ctypes.c_uint32(unit), 3, _fp(res[0]), _fp(res[1]),
+                                    _fp(res[2]), _fp(res[3]), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return res
+
+
+def ref_reflectance_double(name, params, dout, component=3, unit=0):
+    """(3, N) float64: reflectance(out) from the reference's doubleRGB configuration."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n = dout.shape[1]
+    res = np.zeros((3, n), np.float64)
+    rc = lib.bbmref_reflectance_double(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(dout[0]),
+                                       _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component), ctypes.c_uint32(unit),
+                                       _fp(res[0]), _fp(res[1]), _fp(res[2]))
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return res
+
+
 def oracle_models():
     """Models a CPU checker can evaluate on arbitrary inputs: the reference shim if it is present
     (prebuilt in the build container, travels with the tree), else the C restatement."""
@@ -195,6 +228,32 @@ def parity_ok(got, ref, rel_tol=REL_TOL):
         tol = rel_tol * np.maximum(np.abs(ref), FLT_MIN)
         ok = (np.abs(got - ref) <= tol) | (got == ref) | (np.isnan(got) & np.isnan(ref))
     return ok
+
+
+DBL_MIN = float(np.finfo(np.float64).tiny)
+
+
+def parity_ok_f64(got, ref, rel_tol=REL_TOL):
+    """The same bar for doubleRGB outputs: |gpu - ref| <= rel_tol |ref| for every normal double, the absolute step
+    rel_tol DBL_MIN below the normal range, NaN for NaN."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    with np.errstate(invalid="ignore"):
+        tol = rel_tol * np.maximum(np.abs(ref), DBL_MIN)
+        ok = (np.abs(got - ref) <= tol) | (got == ref) | (np.isnan(got) & np.isnan(ref))
+    return ok
+
+
+def rel_err_f64(got, ref):
+    """Element-wise relative error of float64 results (exact agreement = 0)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    same = (got == ref) | (np.isnan(got) & np.isnan(ref))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        err = np.abs(got - ref) / np.maximum(np.abs(ref), DBL_MIN)
+    err[same] = 0.0
+    err[np.isnan(err)] = np.inf
+    return err
 
 
 def parity_violations(got, ref, rel_tol=REL_TOL):

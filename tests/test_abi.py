@@ -44,7 +44,23 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 6
+    assert lib.bbm_hip_abi_version() == 7
+
+
+def test_f64_registry(lib):
+    """doubleRGB kernels: the microfacet family, the diffuse models and their Aggregate(Lambertian, X) fits."""
+    has = {lib.bbm_hip_model_name(i).decode(): lib.bbm_hip_model_has_f64(i) for i in range(lib.bbm_hip_num_models())}
+    for name in ("Lambertian", "OrenNayar", "CookTorrance", "GGX", "CookTorranceHeitz", "Ribardiere",
+                 "LowMicrofacetFit", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,NganCookTorrance>"):
+        assert has[name] == 1, name
+    for name in ("HeWestin", "EPD", "Bagher", "Ward", "Merl"):
+        assert has[name] == 0, name
+    assert lib.bbm_hip_model_has_f64(10_000) == -1
+    # a model without doubleRGB kernels is refused before anything is launched
+    p = (ctypes.c_double * 7)()
+    mid = lib.bbm_hip_model_id(b"HeWestin")
+    assert lib.bbm_hip_eval_pdf_f64(mid, p, 8, None, None, None, None, None, None, None, 0, 3, 0,
+                                    None, None, None, None, None) == -3
 
 
 def test_registry_matches_reference(lib):

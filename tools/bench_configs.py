@@ -1,4 +1,4 @@
-"""bench.py --workload models|sample|fit: BASELINE.json configs 3-5 (one JSON line each).
+"""bench.py --workload models|sample|fit|f64: BASELINE.json configs 3-5 and the doubleRGB path (one JSON line each).
 
   models  (config 3) every single bsdfmodel's eval over 10M shared pairs per GPU, one launch per model
           (bbm_hip_eval).  Algorithmic bytes: 24 B in + 12 B RGB out = 36 B/pair (models that read only
@@ -13,6 +13,8 @@
           reference (a MERL .binary holding a perturbed Bagher fit, read through bbm_amd.Merl) on the MERL grid (90 x 90 x 180 = 1.458M pairs, sharded over the GPUs),
           2P = 36 probes in one bbm_hip_loss launch, plus the RCCL all-reduce of the 36 partial sums
           when N > 1 (strong scaling: the grid is fixed).  Reported as probe-pair evaluations/s.
+  f64     the doubleRGB configuration (bbm_hip_eval_pdf_f64): --model's eval+pdf over --pairs f64 pairs per GPU, 80 B
+          per pair algorithmic (48 B in + 32 B out), and every model with doubleRGB kernels over 10M shared pairs.
 Timing follows bench.py: warmup, barrier + synchronize around K timed steps, max over ranks.
 """
 import ctypes
@@ -220,5 +222,50 @@ def bench_fit(args, dist, rank, world):
                "roofline": valu_roofline("fit:Aggregate", kern_ms, len(probes) * (pairs // world))})
 
 
+def bench_f64(args, dist, rank, world):
+    """doubleRGB (bbm_hip_eval_pdf_f64): --model's eval+pdf over --pairs f64 pairs per GPU (HIP-event timed, HBM
+    roofline at 80 B/pair: 48 B in + 32 B out), and every doubleRGB model over 10M shared pairs (graph-timed)."""
+    begin, n = bh.shard(args.pairs, rank, world, args.scaling)
+    din = bbm_amd.fill_directions(SEED, 0, begin, n, mode=0).double()
+    dout = bbm_amd.fill_directions(SEED, 1, begin, n, mode=0).double()
+    rgb = torch.empty((3, n), dtype=torch.float64, device="cuda")
+    pdf = torch.empty((n,), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream()
+    model = bbm_amd.BsdfModel(args.model)
+    elapsed, kern_ms = _timed(lambda: model.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=stream), args, dist, stream)
+    ok = bool(torch.isfinite(pdf).all()) and float(rgb[0].abs().max()) > 0
+    bpp = 80
+    gbs = bpp * n / (kern_ms * 1e-3) / 1e9
+    del din, dout, rgb, pdf
+    m10 = 10_000_000
+    din = bbm_amd.fill_directions(SEED, 0, rank * m10, m10, mode=0).double()
+    dout = bbm_amd.fill_directions(SEED, 1, rank * m10, m10, mode=0).double()
+    rgb = torch.empty((3, m10), dtype=torch.float64, device="cuda")
+    pdf = torch.empty((m10,), dtype=torch.float64, device="cuda")
+    per = {}
+    lib = _lib.load()
+    for name in _subset(args, [m for i, m in enumerate(bbm_amd.model_names()) if lib.bbm_hip_model_has_f64(i) == 1]):
+        mm = bbm_amd.BsdfModel(name)
+        graph = _graph(lambda s: mm.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=s), GRAPH_REPS)
+        _, step_ms = _timed(graph.replay, args, dist, stream)
+        k = step_ms / GRAPH_REPS
+        per[name] = {"kernel_ms": k, "pairs_per_s": m10 / (k * 1e-3), "GB_s": bpp * m10 / (k * 1e-3) / 1e9,
+                     "roofline_frac": bpp * m10 / (k * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if rank == 0:
+        global_pairs = n * world if args.scaling == "weak" else args.pairs
+        d = {"metric": f"BSDF evals/s (eval+pdf), {args.model}, doubleRGB (f64)", "value": global_pairs * args.steps / elapsed,
+             "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+             "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": args.scaling,
+             "vs_baseline": None, "dtype": "f64", "data": "synthetic (counter-based directions, widened to f64 on device)",
+             "config": {"workload": f"{args.model} fused eval+pdf, {n} pairs per GPU, f64 SoA (doubleRGB)",
+                        "pairs_per_gpu": n, "parallelism": f"dp{world} (independent shards, no collective)"},
+             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": gbs / HBM_PEAK_GBS, "traffic": None, "kernel": f"k_eval_pdf_f64<{args.model}>",
+                          "kernel_ms": kern_ms, "bytes_per_pair": bpp},
+             "outputs_ok": ok, "per_model_10M": per}
+        print(json.dumps(d), flush=True)
+
+
 def run(args, dist, rank, world):
-    {"models": bench_models, "sample": bench_sample, "fit": bench_fit}[args.workload](args, dist, rank, world)
+    {"models": bench_models, "sample": bench_sample, "fit": bench_fit, "f64": bench_f64}[args.workload](
+        args, dist, rank, world)
