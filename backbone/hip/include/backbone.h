@@ -63,8 +63,8 @@ namespace bbm {
       using Spectrum = backbone::color<LANE>;
       static constexpr string_literal name = LABEL;
 
-      //! \brief the device kernels evaluate this configuration: every model in f32 (floatRGB), the microfacet
-      //! family, the diffuse models and their Aggregate(Lambertian, X) fits in f64 (doubleRGB, bbm_hip_*_f64)
+      //! \brief the device kernels evaluate this configuration: every model in f32 (floatRGB); in f64 (doubleRGB,
+      //! bbm_hip_*_f64) every analytic model but Bagher, EPD and the He family, and their Aggregate(Lambertian, X) fits
       static constexpr bool device_batch = std::is_same_v<LANE, float> || std::is_same_v<LANE, double>;
 
       static Spectrum wavelength(void) { return {0.645, 0.526, 0.444}; }

@@ -568,7 +568,7 @@ namespace bbm {
 
     //! \brief doubleRGB (Value = double) models on f64 SoA arrays: eval + pdf, evaluated in f64 on the device
     //! (bbm_hip_eval_pdf_f64).  MODEL must have a single kernel (single model or fused aggregate) with doubleRGB
-    //! kernels (bbm_hip_model_has_f64: Lambertian, OrenNayar, the microfacet compositions and their
+    //! kernels (bbm_hip_model_has_f64: every analytic model but Bagher, EPD and the He family, and their
     //! Aggregate(Lambertian, X) fits); any other model is rejected with BBM_HIP_ERR_UNSUPPORTED.
     template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
       inline void eval_pdf(const MODEL& model, soa3d in, soa3d out, size_t n, soa3d_out rgb, double* p,
@@ -579,6 +579,19 @@ namespace bbm {
       const std::vector<double> prm = parameters_f64(model);
       check(bbm_hip_eval_pdf_f64(id, prm.data(), int(prm.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
                                  uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, p, stream));
+    }
+
+    //! \brief doubleRGB sample of N (out, xi) -> direction, pdf, flag (bbm_hip_sample_f64)
+    template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
+      inline void sample(const MODEL& model, soa3d out, const double* xi0, const double* xi1, size_t n,
+                         soa3d_out direction, double* p, uint32_t* flag,
+                         bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                         const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      static const int id = id_of(detail::single_name<MODEL>());
+      const std::vector<double> prm = parameters_f64(model);
+      check(bbm_hip_sample_f64(id, prm.data(), int(prm.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
+                               uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, p, flag, stream));
     }
 
     //! \brief doubleRGB reflectance of N out directions (bbm_hip_reflectance_f64)

@@ -41,6 +41,7 @@ SIGNATURES = {
     "bbm_hip_reflectance": (_I, [_I, _P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
     "bbm_hip_model_has_f64": (_I, [_I]),
     "bbm_hip_eval_pdf_f64": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
+    "bbm_hip_sample_f64": (_I, [_I, _P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
     "bbm_hip_reflectance_f64": (_I, [_I, _P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
     "bbm_hip_fill_directions": (_I, [_U64, _U32, _U64, _SZ, _I, _P, _P, _P, _P]),
     "bbm_hip_model_param_attrs": (_I, [_I, _P, _I]),

@@ -336,10 +336,14 @@ class BsdfModel:
         """Value pdf(in, out, component, unit, mask) for N pairs -> (N,)."""
         return self.eval_pdf(in_, out, component, unit, mask, mode=2, **kw)[1]
 
-    def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
-        """BsdfSample sample(out, xi, component, unit, mask) for N (out, xi) -> BsdfSample."""
+    def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None,
+               params64=None):
+        """BsdfSample sample(out, xi, component, unit, mask) for N (out, xi) -> BsdfSample (float64 out / xi: the
+        doubleRGB kernels, float64 direction and pdf)."""
         torch = _torch()
-        ox, oy, oz, n = _soa(out, what="out")
+        f64 = _is_f64(out)
+        dt = torch.float64 if f64 else torch.float32
+        ox, oy, oz, n = _soa(out, what="out", dtype=dt)
         if isinstance(xi, (tuple, list)):
             x0, x1 = xi
         else:
@@ -347,19 +351,23 @@ class BsdfModel:
                 raise ValueError("xi: expected a (2, N) tensor")
             x0, x1 = xi[0], xi[1]
         for x in (x0, x1):
-            if x.dtype != torch.float32 or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
-                raise TypeError("xi: expected float32 CUDA rows with one entry per direction")
+            if x.dtype != dt or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
+                raise TypeError(f"xi: expected {str(dt).replace('torch.', '')} CUDA rows with one entry per direction")
         mptr, _keep = _mask_ptr(mask, n)
         dev = x0.device
-        d = torch.empty((3, n), dtype=torch.float32, device=dev)
-        p = torch.empty((n,), dtype=torch.float32, device=dev)
+        d = torch.empty((3, n), dtype=dt, device=dev)
+        p = torch.empty((n,), dtype=dt, device=dev)
         f = torch.empty((n,), dtype=torch.int32, device=dev)
         _on_stream(stream, _keep, d, p, f)
         lib = _lib.load()
-        _lib.check(lib.bbm_hip_sample(self.model_id, self._pptr(), self._params.size, ox, oy, oz,
-                                      x0.data_ptr(), x1.data_ptr(), mptr, n, int(component), int(unit),
-                                      d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
-                                      _stream_ptr(stream)))
+        if f64:
+            prm = self._params_f64(params64)
+            fn, pp, npar = lib.bbm_hip_sample_f64, prm.ctypes.data_as(ctypes.c_void_p), prm.size
+        else:
+            fn, pp, npar = lib.bbm_hip_sample, self._pptr(), self._params.size
+        _lib.check(fn(self.model_id, pp, npar, ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
+                      int(unit), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
+                      _stream_ptr(stream)))
         return BsdfSample(d, p, f)
 
     def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None,

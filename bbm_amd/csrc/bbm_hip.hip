@@ -659,6 +659,30 @@ int bbm_hip_eval_pdf_f64(int model_id, const double* params, int nparams,
   return l->eval_pdf(a, static_cast<hipStream_t>(stream));
 }
 
+int bbm_hip_sample_f64(int model_id, const double* params, int nparams,
+                       const double* out_x, const double* out_y, const double* out_z,
+                       const double* xi0, const double* xi1,
+                       const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                       double* dir_x, double* dir_y, double* dir_z, double* pdf, uint32_t* flag, void* stream)
+{
+  (void)unit;
+  const ModelEntry* e;
+  const f64::F64Launchers* l;
+  f64::SampleArgsF64 a;
+  std::memset(&a, 0, sizeof(a));
+  int rc = prepare_f64(model_id, params, nparams, e, l, a.p);
+  if (rc) return rc;
+  if (n == 0) return BBM_HIP_OK;
+  if (!out_x || !out_y || !out_z) return fail(BBM_HIP_ERR_INVALID_ARG, "out direction pointer is NULL");
+  if (!xi0 || !xi1) return fail(BBM_HIP_ERR_INVALID_ARG, "xi pointer is NULL");
+  if (!dir_x || !dir_y || !dir_z || !pdf || !flag) return fail(BBM_HIP_ERR_INVALID_ARG, "sample output pointer is NULL");
+  a.ox = out_x; a.oy = out_y; a.oz = out_z; a.xi0 = xi0; a.xi1 = xi1; a.mask = mask;
+  a.dx = dir_x; a.dy = dir_y; a.dz = dir_z; a.pdf = pdf; a.flag = flag;
+  a.n = n;
+  a.component = component & kFlagAll;
+  return l->sample(a, static_cast<hipStream_t>(stream));
+}
+
 int bbm_hip_reflectance_f64(int model_id, const double* params, int nparams,
                             const double* out_x, const double* out_y, const double* out_z,
                             const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,

@@ -81,6 +81,21 @@ __global__ __launch_bounds__(kBlock) void k_reflectance_f64(ReflArgsF64 a)
   }
 }
 
+template<class Model, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_sample_f64(SampleArgsF64 a)
+{
+  const Model m(a.p.v);
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
+  {
+    d3 d;
+    double pdf;
+    uint32_t f;
+    m.sample(mk(a.ox[i], a.oy[i], a.oz[i]), a.xi0[i], a.xi1[i], (!MASK || a.mask[i]) ? a.component : 0u, d, pdf, f);
+    a.dx[i] = d.x; a.dy[i] = d.y; a.dz[i] = d.z; a.pdf[i] = pdf; a.flag[i] = f;
+  }
+}
+
 unsigned grid(uint64_t units)
 {
   const uint64_t b = (units + kBlock - 1) / kBlock;
@@ -95,12 +110,19 @@ int launched(const char* what)
   return (e == hipSuccess) ? 0 : fail(BBM_HIP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Grid cap (0 = full grid): the Student-T NDF's per-thread setup (two f64 tgamma and a pow) is amortised over
+// several grid-stride iterations (the floatRGB kernels' eval_grid_cap, kernels.hpp)
+template<class Model> struct grid_cap { static constexpr unsigned value = 0; };
+template<> struct grid_cap<RibardiereM> { static constexpr unsigned value = 2048; };
+template<> struct grid_cap<RibardiereAnisoM> { static constexpr unsigned value = 2048; };
+
 template<class Model>
 int launch_eval_pdf(const EvalArgsF64& a, hipStream_t s)
 {
   const bool v2 = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
                   aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
-  const unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
+  unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
+  if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
   if (v2 && a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (v2) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true>), dim3(blocks), dim3(kBlock), 0, s, a);
@@ -116,8 +138,18 @@ int launch_reflectance(const ReflArgsF64& a, hipStream_t s)
   return launched("k_reflectance_f64");
 }
 
+template<class Model>
+int launch_sample(const SampleArgsF64& a, hipStream_t s)
+{
+  unsigned blocks = grid(a.n);
+  if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
+  if (a.mask) hipLaunchKernelGGL((k_sample_f64<Model, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_sample_f64<Model, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+  return launched("k_sample_f64");
+}
+
 struct Entry { const char* name; F64Launchers l; };
-#define BBM_HIP_F64(NAME, M) {NAME, {&launch_eval_pdf<M>, &launch_reflectance<M>}}
+#define BBM_HIP_F64(NAME, M) {NAME, {&launch_eval_pdf<M>, &launch_reflectance<M>, &launch_sample<M>}}
 // names as in the floatRGB registry (bbm_hip.hip); aliases share a composition as they do there
 const Entry kF64[] = {
   BBM_HIP_F64("Lambertian", Lambertian),
@@ -139,13 +171,37 @@ const Entry kF64[] = {
   BBM_HIP_F64("Aggregate<Lambertian,GGX>", AggGGXM),
   BBM_HIP_F64("Aggregate<Lambertian,NganCookTorrance>", AggNganCookTorranceM),
   BBM_HIP_F64("Aggregate<Lambertian,LowMicrofacetFit>", AggLowMicrofacetM),
+  BBM_HIP_F64("Ward", WardM),
+  BBM_HIP_F64("WardDuer", WardDuerM),
+  BBM_HIP_F64("WardDuerGeislerMoroder", WardDGMM),
+  BBM_HIP_F64("NganWard", NganWardM),
+  BBM_HIP_F64("NganWardDuer", NganWardDuerM),
+  BBM_HIP_F64("Phong", PhongLobe),
+  BBM_HIP_F64("NganBlinnPhong", PhongLobe),   // ngan.h:43-44
+  BBM_HIP_F64("Lafortune", LafortuneM),
+  BBM_HIP_F64("NganLafortune", NganLafortuneM),
+  BBM_HIP_F64("AshikhminShirley", ASM),
+  BBM_HIP_F64("AshikhminShirleyFull", ASFullM),
+  BBM_HIP_F64("LowAshikhminShirley", LowASM),
+  BBM_HIP_F64("NganAshikhminShirley", NganASM),
+  BBM_HIP_F64("LowSmooth", LowSmooth),
+  BBM_HIP_F64("Aggregate<Lambertian,LowAshikhminShirley>", AggLowASM),
+  BBM_HIP_F64("Aggregate<Lambertian,LowSmooth>", AggLowSmoothM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganAshikhminShirley>", AggNganASM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganBlinnPhong>", AggPhongM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganLafortune>", AggNganLafortuneM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganWard>", AggNganWardM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganWardDuer>", AggNganWardDuerM),
 };
 #undef BBM_HIP_F64
 
 static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranceM::kParams == 5 && GGXM::kParams == 5 &&
               CookTorranceHeitzM::kParams == 6 && GGXHeitzM::kParams == 6 && NganCookTorranceM::kParams == 5 &&
               PhongWalterM::kParams == 5 && RibardiereM::kParams == 6 && RibardiereAnisoM::kParams == 7 &&
-              LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8, "f64 nparams must match the floatRGB registry");
+              LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8 && WardM::kParams == 5 &&
+              NganWardM::kParams == 4 && PhongLobe::kParams == 4 && LafortuneM::kParams == 7 &&
+              NganLafortuneM::kParams == 6 && ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 &&
+              NganASM::kParams == 5 && LowSmooth::kParams == 6, "f64 nparams must match the floatRGB registry");
 
 }  // namespace
 

@@ -9,7 +9,8 @@
 //
 // Covered compositions: Lambertian, OrenNayar, every microfacet<NDF, G, F, N> composition of the floatRGB
 // registry (Beckmann / GGX / Phong / Student-T / Low NDFs x v-groove / uncorrelated / height-correlated x Cook /
-// Schlick Fresnel) and Aggregate(Lambertian, X) of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
+// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth) and the
+// Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
 // thread with 16 B loads: 48 B in + 32 B out = 80 B per eval+pdf pair.
 #pragma once
 #include "math.hpp"
@@ -36,6 +37,42 @@ __device__ __forceinline__ double tan_theta(d3 v) { return sqrt(sin_theta2(v)) /
 __device__ __forceinline__ double tan_theta2(d3 v) { return sin_theta2(v) / (v.z * v.z); }   // spherical.h:186
 __device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
 
+__device__ __forceinline__ d3 cross(d3 a, d3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+__device__ __forceinline__ bool xi_ok(double xi0, double xi1) { return (xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1); }
+// spherical.h:156-161 cossinPhi: (1, 0) at the pole, else clamp(xy / sinTheta, -1, 1)
+__device__ __forceinline__ void cossin_phi(d3 v, double& c, double& s)
+{
+  const double sT = sqrt(sin_theta2(v));
+  const double r = 1.0 / sT;
+  const bool pole = fabs(sT) < kEps;
+  c = pole ? 1.0 : fmin(fmax(v.x * r, -1.0), 1.0);
+  s = pole ? 0.0 : fmin(fmax(v.y * r, -1.0), 1.0);
+}
+// the native backbone's erfinv (backbone/native/include/backbone/math.h:115-120, Giles' polynomials) in double
+__device__ __forceinline__ double erfinv(double a)
+{
+  const double w = -log((1.0 - a) * (1.0 + a));
+  double p;
+  if (w < 5)
+  {
+    const double x = w - 2.5;
+    p = 2.81022636e-08;
+    p = p * x + 3.43273939e-07; p = p * x + -3.5233877e-06; p = p * x + -4.39150654e-06;
+    p = p * x + 0.00021858087; p = p * x + -0.00125372503; p = p * x + -0.00417768164;
+    p = p * x + 0.246640727; p = p * x + 1.50140941;
+  }
+  else
+  {
+    const double x = sqrt(w) - 3.0;
+    p = -0.000200214257;
+    p = p * x + 0.000100950558; p = p * x + 0.00134934322; p = p * x + -0.00367342844;
+    p = p * x + 0.00573950773; p = p * x + -0.0076224613; p = p * x + 0.00943887047;
+    p = p * x + 1.00167406; p = p * x + 2.83297682;
+  }
+  return p * a;
+}
+constexpr double kInvSqrtPi = 0.56418958354775627928034964497783221304416656494140625;   // std::numbers::inv_sqrtpi
+
 // Walter's rational approximation of the Smith G1 (beckmann.h:195, phong.h G1)
 __device__ __forceinline__ double walter_g1(double a) { return (a < 1.6) ? (3.535 * a + 2.181 * a * a) / (1 + 2.276 * a + 2.577 * a * a) : 1.0; }
 
@@ -61,6 +98,31 @@ struct Beckmann
     const double a = Aniso ? 1.0 / sqrt(sqnorm2(v.x * au, v.y * av) / (v.z * v.z)) : 1.0 / (au * tan_theta(v));
     return mask ? walter_g1(a) : 0.0;
   }
+  // beckmann.h:76-116: visible normals after [Jakob 2014] (stretch, three Newton steps on erfinv, rotate, unstretch)
+  __device__ __forceinline__ d3 sample(d3 view, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    const d3 vs = normalize(mk(view.x * au, view.y * av, view.z));
+    const double tanT = tan_theta(vs);
+    const double maxval = erf(1.0 / tanT);
+    double xc0 = fmin(fmax(xi0, 10e-6), 1.0 - 10e-6);
+    const double xc1 = fmin(fmax(xi1, 10e-6), 1.0 - 10e-6);
+    double x = maxval - (maxval + 1) * erf(sqrt(-log(xc0)));
+    xc0 *= 1.0 + maxval + kInvSqrtPi * tanT * exp(-(vs.z * vs.z));
+    for (int i = 0; i < 3; ++i)
+    {
+      const double slope = erfinv(x);
+      const double val = 1.0 + x + kInvSqrtPi * tanT * exp(-slope * slope) - xc0;
+      const double der = 1.0 - slope * tanT;
+      x -= val / der;
+    }
+    double s0 = 0.0, s1 = 0.0;
+    if (x > -1.0 && x < +1.0) { s0 = erfinv(x); s1 = erfinv(2.0 * xc1 - 1.0); }
+    double c, s;
+    cossin_phi(vs, c, s);
+    const double u0 = (c * s0 + -s * s1) * au, u1 = (s * s0 + c * s1) * av;
+    return normalize(mk(-u0, -u1, 1.0));
+  }
 };
 
 // ndf::ggx (include/ndf/ggx.h:50-65 eval, :173-189 G1)
@@ -82,6 +144,24 @@ struct GGX
     const double denom = 1.0 + sqrt(1.0 + (au * av) * tan_theta2(v));
     return mask ? 2.0 / denom : 0.0;
   }
+  // ggx.h:84-108: visible normals after [Heitz 2017]
+  __device__ __forceinline__ d3 sample(d3 view, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    const d3 vs = normalize(mk(view.x * au, view.y * av, view.z));
+    const d3 T1 = (vs.z < 1.0 - kEps) ? normalize(cross(vs, mk(0.0, 0.0, 1.0))) : mk(1.0, 0.0, 0.0);
+    const d3 T2 = cross(T1, vs);
+    const double a = 1.0 / (1.0 + vs.z);
+    const double r = sqrt(xi0);
+    const double phi = ((xi1 < a) ? xi1 / a : 1.0 + (xi1 - a) / (1.0 - a)) * kPi;
+    double sp, cp;
+    sincos(phi, &sp, &cp);
+    const double P1 = r * cp;
+    const double P2 = ((xi1 < a) ? 1.0 : vs.z) * r * sp;
+    const double sq = safe_sqrt(1.0 - P1 * P1 - P2 * P2);
+    const d3 n = mk((P1 * T1.x + P2 * T2.x) + sq * vs.x, (P1 * T1.y + P2 * T2.y) + sq * vs.y, (P1 * T1.z + P2 * T2.z) + sq * vs.z);
+    return normalize(mk(n.x * au, n.y * av, fmax(0.0, n.z)));
+  }
 };
 
 // ndf::phong (include/ndf/phong.h:31-140): D = (s + 2) / (2 pi) cos^s, pdf = D cos, Walter's G1 rational
@@ -101,6 +181,16 @@ struct PhongNdf
     return mask ? walter_g1(sqrt(0.5 * sharpness + 1) / tan_theta(v)) : 0.0;
   }
   __device__ __forceinline__ double pdf(d3, d3 m, double D) const { return (m.z > 0) ? D * fabs(m.z) : 0.0; }
+  // phong.h:64-79
+  __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    const double cosT = pow(xi0, 1.0 / (sharpness + 2));
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    double sp, cp;
+    sincos(xi1 * (2.0 * kPi), &sp, &cp);
+    return mk(cp * sinT, sp * sinT, cosT);
+  }
 };
 
 // ndf::studentt (include/ndf/studentt.h:34-195), Ribardiere et al. 2017
@@ -112,7 +202,7 @@ struct StudentT
   __device__ explicit StudentT(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]), gamma(p[Aniso ? 2 : 1])
   {
     // parameter-only factors of G1 (studentt.h:152-156), once per thread
-    lam_scale = tgamma(gamma - 0.5) / tgamma(gamma) * 0.56418958354775627928034964497783221304416656494140625;
+    lam_scale = tgamma(gamma - 0.5) / tgamma(gamma) * kInvSqrtPi;
     s1_scale = pow(gamma - 1, gamma) / (2 * gamma - 3);
     sqrt_g1 = sqrt(gamma - 1);
     f22 = F22(gamma);
@@ -161,6 +251,25 @@ struct StudentT
     const double p = D * m.z;
     return ((m.z > 0) && (p > 0)) ? p : 0.0;
   }
+  // studentt.h:67-90
+  __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    double sp, cp;
+    sincos((2.0 * kPi) * xi0, &sp, &cp);
+    double normalization;
+    if (Aniso)
+    {
+      normalization = 1.0 / sqnorm2(cp / au, sp / av);
+      const double x = cp * au, y = sp * av, r = 1.0 / sqrt(x * x + y * y);
+      cp = x * r; sp = y * r;
+    }
+    else normalization = au * au;
+    const double tan2 = (pow(xi1, 1.0 / (1.0 - gamma)) - 1) * (gamma - 1) * normalization;
+    const double cosT = 1.0 / sqrt(1.0 + tan2);
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    return mk(cp * sinT, sp * sinT, cosT);
+  }
 };
 
 // ndf::low (include/ndf/low.h:32-141): the ABC "S" term as an NDF; G1 = 1
@@ -172,6 +281,17 @@ struct LowNdf
   {
     const double normalization = (fabs(C - 1) < kEps) ? 1.0 / log(1.0 + B) : (C - 1.0) / (1.0 - pow(1.0 + B, 1.0 - C));
     norm_pdf = 0.5 * kInvPi * normalization;
+  }
+  // low.h:67-89: inverse of the marginal CDF of cos(theta)
+  __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    const double term = (fabs(C - 1) < kEps) ? exp(xi0 * log(1.0 + B)) : pow(1.0 + xi0 * (pow(1.0 + B, 1.0 - C) - 1.0), -1.0 / (C - 1.0));
+    const double cosT = (1.0 + B - term) / B;
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    double sp, cp;
+    sincos(xi1 * (2.0 * kPi), &sp, &cp);
+    return mk(cp * sinT, sp * sinT, cosT);
   }
   __device__ __forceinline__ double eval(d3 h) const { return (h.z > 0) ? pow(1.0 + B * (1.0 - h.z), -C) : 0.0; }
   __device__ __forceinline__ double G1(d3, d3) const { return 1.0; }
@@ -299,6 +419,23 @@ struct Microfacet
     pdf = active ? ndf_pdf<NDF>::run(ndf, out, h, D) / (4.0 * fabs(outh)) : 0.0;
   }
 
+  // :115-141: m ~ NDF sample(out), direction = reflect(out, m) = m (m.out) 2.0 - out (core/vec_transform.h:43-44),
+  // pdf = pdf(direction, out), flag Specular
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk(0.0, 0.0, 0.0);
+    pdf = 0.0;
+    flag = kFlagNone;
+    if (!(component & kFlagSpecular) || !xi_ok(xi0, xi1) || !(out.z > 0)) return;
+    const d3 m = ndf.sample(out, xi0, xi1);
+    const double d = dot(m, out);
+    dir = mk(m.x * d * 2.0 - out.x, m.y * d * 2.0 - out.y, m.z * d * 2.0 - out.z);
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+
   // :182-196 mirror approximation Fresnel(eta, z(out)) / N * 4.0, x albedo
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
@@ -328,6 +465,22 @@ struct Lambertian
     const bool m = component & kFlagDiffuse;
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0;
+  }
+  // lambertian.h:76-103: cosine-weighted directions
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk(0.0, 0.0, 0.0);
+    pdf = 0.0;
+    flag = kFlagNone;
+    if (!(component & kFlagDiffuse) || !xi_ok(xi0, xi1)) return;
+    double s, c;
+    sincos(xi0 * (2.0 * kPi), &s, &c);
+    const double sinT = safe_sqrt(1.0 - xi1);
+    dir = mk(c * sinT, s * sinT, safe_sqrt(xi1));
+    const bool m = (dir.z >= 0) && (out.z >= 0);
+    pdf = m ? dir.z * kInvPi : 0.0;
+    flag = kFlagDiffuse;
   }
 };
 
@@ -359,6 +512,12 @@ struct OrenNayar
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0;
   }
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    const double one[3] = {1.0, 1.0, 1.0};
+    Lambertian(one).sample(out, xi0, xi1, component, dir, pdf, flag);
+  }
 };
 
 // aggregatemodel<A, B> (bsdfmodel/aggregatemodel.h:60-163): eval and reflectance sum (right folds of two
@@ -378,12 +537,44 @@ struct Aggregate
     b.eval_pdf(in, out, component, rb, pb);
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = ra[c] + rb[c];
+    double wa, wb;
+    weights(out, component, wa, wb);
+    pdf = component ? mix(pa, pb, wa, wb) : 0.0;
+  }
+  // hsum(reflectance(out)) per child (horizontal.h:64-67)
+  __device__ __forceinline__ void weights(d3 out, uint32_t component, double& wa, double& wb) const
+  {
+    double ra[3], rb[3];
     a.reflectance(out, component, ra);
     b.reflectance(out, component, rb);
-    const double wa = ((0.0 + ra[0]) + ra[1]) + ra[2], wb = ((0.0 + rb[0]) + rb[1]) + rb[2];
+    wa = ((0.0 + ra[0]) + ra[1]) + ra[2];
+    wb = ((0.0 + rb[0]) + rb[1]) + rb[2];
+  }
+  // inner_product(pdfs, weights, 0) / sum, masked sum > eps (:141-142)
+  __device__ __forceinline__ static double mix(double pa, double pb, double wa, double wb)
+  {
     const double sum = (0.0 + wa) + wb;
     const double ip = (0.0 + pa * wa) + pb * wb;
-    pdf = (component && sum > kEps) ? ip / sum : 0.0;
+    return (sum > kEps) ? ip / sum : 0.0;
+  }
+  // :81-113: the child claiming xi0 * sum (a later child that also claims it wins), pdf of the mixture
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk(0.0, 0.0, 0.0);
+    pdf = 0.0;
+    flag = kFlagNone;
+    if (!component) return;
+    double wa, wb, p;
+    weights(out, component, wa, wb);
+    double x = xi0 * ((0.0 + wa) + wb);
+    if ((x >= 0) && (x <= wa)) a.sample(out, (wa > kEps) ? x / wa : 0.0, xi1, component, dir, p, flag);
+    x -= wa;
+    if ((x >= 0) && (x <= wb)) b.sample(out, (wb > kEps) ? x / wb : 0.0, xi1, component, dir, p, flag);
+    double rgb[3], pa, pb;
+    a.eval_pdf(dir, out, component, rgb, pa);
+    b.eval_pdf(dir, out, component, rgb, pb);
+    pdf = mix(pa, pb, wa, wb);
   }
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
@@ -394,6 +585,382 @@ struct Aggregate
     for (int c = 0; c < 3; ++c) rgb[c] = ra[c] + rb[c];
   }
 };
+
+// ------------------------------------------------------------------------------------------ lobe models
+
+__device__ __forceinline__ d3 reflect(d3 out, d3 m)     // core/vec_transform.h:43-44
+{
+  const double d = dot(m, out);
+  return mk(m.x * d * 2.0 - out.x, m.y * d * 2.0 - out.y, m.z * d * 2.0 - out.z);
+}
+
+// toGlobalShadingFrame(normal) * v (core/shading_frame.h:24-48, Duff et al. 2017)
+__device__ __forceinline__ d3 to_global(d3 normal, d3 v)
+{
+  const d3 Z = normalize(normal);
+  const double sign = copysign(1.0, Z.z);
+  const double a = -1.0 / (sign + Z.z);
+  const double b = Z.x * Z.y * a;
+  const d3 X = mk(1.0 + sign * Z.x * Z.x * a, sign * b, -sign * Z.x);
+  const d3 Y = mk(b, sign + Z.y * Z.y * a, -Z.y);
+  return mk(((0.0 + X.x * v.x) + Y.x * v.y) + Z.x * v.z, ((0.0 + X.y * v.x) + Y.y * v.y) + Z.y * v.z,
+            ((0.0 + X.z * v.x) + Y.z * v.y) + Z.z * v.z);
+}
+
+#define BBM_F64_SAMPLE_PROLOGUE                          \
+  dir = mk(0.0, 0.0, 0.0); pdf = 0.0; flag = kFlagNone;  \
+  if (!((component & kFlagSpecular) && xi_ok(xi0, xi1))) return;
+
+// Ward (ward.h:26-168, KIND 0), Ward-Duer (wardduer.h:29-81, KIND 1), Ward-Duer-Geisler-Moroder
+// (wardduergeislermoroder.h:29-81, KIND 2); isotropic: NganWard / NganWardDuer (ngan.h:30-38)
+template<int KIND, bool Aniso>
+struct Ward
+{
+  static constexpr int kParams = 3 + (Aniso ? 2 : 1);
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double albedo[3], rx, ry;
+  __device__ explicit Ward(const double* p) : rx(p[3]), ry(Aniso ? p[4] : p[3]) { albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2]; }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
+    const d3 H = mk(in.x + out.x, in.y + out.y, in.z + out.z);
+    const double zH2 = H.z * H.z;
+    const double exponent = sqnorm2(H.x / rx, H.y / ry) / zH2;
+    double nf;
+    if (KIND == 0) nf = 4.0 * kPi * sqrt(in.z * out.z) * rx * ry;
+    else if (KIND == 1) nf = 4.0 * kPi * rx * ry * (in.z * out.z);
+    else nf = 4.0 * kPi * rx * ry * (zH2 * zH2) / dot(H, H);
+    const double f = exp(-exponent) / nf;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = active ? albedo[c] * f : 0.0;
+    // ward.h:126-140
+    const d3 h = normalize(H);
+    const double np = 4.0 * kPi * rx * ry * dot(in, h) * (h.z * h.z * h.z);
+    pdf = active ? exp(-(sqnorm2(h.x / rx, h.y / ry) / (h.z * h.z))) / np : 0.0;
+  }
+  __device__ __forceinline__ void reflectance(d3, uint32_t component, double* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0;
+  }
+  // ward.h:90-110
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    BBM_F64_SAMPLE_PROLOGUE
+    double s, c;
+    sincos(2.0 * kPi * xi0, &s, &c);
+    const double cx = c * rx, cy = s * ry, r = 1.0 / sqrt(sqnorm2(cx, cy));
+    const double csx = cx * r, csy = cy * r;
+    const double cosT = 1.0 / sqrt(1.0 - (log(xi1) / sqnorm2(csx / rx, csy / ry)));
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    dir = reflect(out, mk(csx * sinT, csy * sinT, cosT));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+
+// Phong lobe about reflect(in) (bsdfmodel/phong.h:25-163; NganBlinnPhong, ngan.h:43-44)
+struct PhongLobe
+{
+  static constexpr int kParams = 4;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double albedo[3], s;
+  __device__ explicit PhongLobe(const double* p) : s(p[3]) { albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2]; }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
+    const double pw = pow(fmax(dot(mk(-in.x, -in.y, in.z), out), 0.0), s);
+    const double f = (s + 2) * (0.5 * kInvPi) * pw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = active ? albedo[c] * f : 0.0;
+    pdf = active ? (s + 1) * (0.5 * kInvPi) * pw : 0.0;
+  }
+  __device__ __forceinline__ void reflectance(d3, uint32_t component, double* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? albedo[c] : 0.0;
+  }
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    BBM_F64_SAMPLE_PROLOGUE
+    double sp, cp;
+    sincos(xi0 * (2.0 * kPi), &sp, &cp);
+    const double cosT = pow(xi1, 1.0 / (s + 1));
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    dir = to_global(mk(-out.x, -out.y, out.z), mk(cp * sinT, sp * sinT, cosT));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+
+// Lafortune (bsdfmodel/lafortune.h:28-172) and Ngan's normalised isotropic lobe (ngan.h:54-129)
+template<bool Aniso, bool NGAN>
+struct Lafortune
+{
+  static constexpr int kParams = 3 + (Aniso ? 2 : 1) + 2;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double albedo[3], cx, cy, cz, s, ngan;
+  __device__ explicit Lafortune(const double* p) : cx(p[3]), cy(Aniso ? p[4] : p[3]), cz(p[Aniso ? 5 : 4]), s(p[Aniso ? 6 : 5])
+  {
+    albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2];
+    ngan = NGAN ? (s + 2.0) * (0.5 * kInvPi) / pow(fmax(cz * cz, cx * cx), s * 0.5) : 1.0;
+  }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool ev = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    const double fr = pow(fmax(dot(mk(cx, cy, cz), mk(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0), s);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = ev ? (NGAN ? albedo[c] * fr * ngan : albedo[c] * fr) : 0.0;
+    const bool pd = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
+    const d3 co = normalize(mk(cx * out.x, cy * out.y, cz * out.z));
+    pdf = pd ? (s + 1) / (2.0 * kPi) * pow(fmax(dot(co, in), 0.0), s) : 0.0;
+  }
+  __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
+  {
+    const bool m = component & kFlagSpecular;
+    const d3 co = mk(cx * out.x, cy * out.y, cz * out.z);
+    const double normalization = pow(sqrt(dot(co, co)), s) * (2.0 * kPi) / (s + 2);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? (NGAN ? albedo[c] * normalization * ngan : albedo[c] * normalization) : 0.0;
+  }
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    BBM_F64_SAMPLE_PROLOGUE
+    double sp, cp;
+    sincos(xi0 * (2.0 * kPi), &sp, &cp);
+    const double cosT = pow(xi1, 1.0 / (s + 1));
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    dir = to_global(mk(cx * out.x, cy * out.y, cz * out.z), mk(cp * sinT, sp * sinT, cosT));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+
+// Schlick with a Spectrum reflectance (fresnel_schlick.h:42-53, per channel); ScalarFresnel3: a scalar Fresnel
+// broadcast to the three channels
+struct FresnelSchlickRGB
+{
+  static constexpr int kParams = 3;
+  double r0[3];
+  __device__ explicit FresnelSchlickRGB(const double* p) { r0[0] = p[0]; r0[1] = p[1]; r0[2] = p[2]; }
+  __device__ __forceinline__ void eval3(double c, double* F) const
+  {
+    const double x5 = pow(1.0 - c, 5.0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] = r0[k] + (1.0 - r0[k]) * x5;
+  }
+  __device__ __forceinline__ double hsum() const { return ((0.0 + r0[0]) + r0[1]) + r0[2]; }
+};
+template<class F>
+struct ScalarFresnel3 : F
+{
+  __device__ explicit ScalarFresnel3(const double* p) : F(p) {}
+  __device__ __forceinline__ void eval3(double c, double* out) const { out[0] = out[1] = out[2] = F::eval(c); }
+};
+
+// Ashikhmin-Shirley (ashikhminshirley.h:29-221), the scaled Low / Ngan variants (low.h:24-25, ngan.h:157-158) and
+// the full model with its coupled diffuse term (ashikhminshirleyfull.h:31-191)
+template<class FRES, bool Aniso, bool SCALED, bool FULL>
+struct AshikhminShirley
+{
+  static constexpr int kOff = (SCALED ? 3 : 0) + (FULL ? 3 : 0);
+  static constexpr int kParams = kOff + FRES::kParams + (Aniso ? 2 : 1);
+  static constexpr uint32_t kComponent = FULL ? kFlagAll : kFlagSpecular;
+  double albedo[3], diffuse[3], su, sv;
+  FRES fres;
+  __device__ explicit AshikhminShirley(const double* p)
+      : su(p[kOff + FRES::kParams]), sv(p[kOff + FRES::kParams + (Aniso ? 1 : 0)]), fres(p + kOff)
+  {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { albedo[k] = SCALED ? p[k] : 1.0; diffuse[k] = FULL ? p[k] : 0.0; }
+  }
+  __device__ __forceinline__ double exponent(d3 h) const
+  {
+    if (!Aniso) return su;
+    return (h.z < 1.0 - kEps) ? (su * (h.x * h.x) + sv * (h.y * h.y)) / (1.0 - h.z * h.z) : 0.0;
+  }
+  // ashikhminshirley.h:148-176
+  __device__ __forceinline__ double spec_pdf(d3 in, d3 out, uint32_t component) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
+    const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
+    const double normalization = Aniso ? sqrt((su + 1) * (sv + 1)) / (2.0 * kPi) : (su + 1.0) / (2.0 * kPi);
+    return active ? normalization * pow(h.z, exponent(h)) / (4.0 * dot(h, in)) : 0.0;
+  }
+  __device__ __forceinline__ double diff_albedo() const
+  {
+    return (((0.0 + diffuse[0]) + diffuse[1]) + diffuse[2]) * (1.0 - fres.hsum());
+  }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool upper = (in.z > 0) && (out.z > 0);
+    const bool spec = (component & kFlagSpecular) && upper;
+    const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
+    const double hdi = dot(h, in);
+    double F[3];
+    fres.eval3(hdi, F);
+    const double normalization = Aniso ? sqrt((su + 1) * (sv + 1)) / (8.0 * kPi) : (su + 1) / (8.0 * kPi);
+    const double np = normalization * pow(h.z, exponent(h));
+    const double denom = hdi * fmax(in.z, out.z);
+    double diff_scale = 0.0;
+    if constexpr (FULL)
+      diff_scale = 28.0 / (23.0 * kPi) * ((1.0 * (1.0 - pow(1.0 - 0.5 * in.z, 5.0))) * (1.0 - pow(1.0 - 0.5 * out.z, 5.0)));
+    const bool diff = FULL && (component & kFlagDiffuse) && upper;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      double v = np * F[c] / denom;
+      if (SCALED) v *= albedo[c];
+      v = spec ? v : 0.0;
+      if constexpr (FULL) v = diff ? (diff_scale * diffuse[c] * (1.0 - fres.r0[c])) + v : v;
+      rgb[c] = upper ? v : 0.0;
+    }
+    const double sp = spec_pdf(in, out, component);
+    if constexpr (FULL)
+    {
+      // ashikhminshirleyfull.h:148-168
+      const double dpdf = ((component & kFlagDiffuse) && (in.z >= 0) && (out.z >= 0)) ? in.z * kInvPi : 0.0;
+      const double da = diff_albedo(), sa = fres.hsum();
+      const double dw = (da > kEps) ? da / (da + sa) : 0.0;
+      const double sw = 1.0 - dw;
+      pdf = !(component & kFlagDiffuse) ? sp : (!(component & kFlagSpecular) ? dpdf : sw * sp + dw * dpdf);
+    }
+    else pdf = sp;
+  }
+  // ashikhminshirley.h:181-190 (+ ashikhminshirleyfull.h:170-185)
+  __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
+  {
+    const bool up = out.z > 0;
+    const bool ms = (component & kFlagSpecular) && up;
+    double F[3];
+    fres.eval3(out.z, F);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      double v = ms ? (SCALED ? F[c] * albedo[c] : F[c]) : 0.0;
+      if constexpr (FULL) v = (up && (component & kFlagDiffuse)) ? diffuse[c] * (1.0 - fres.r0[c]) + v : v;
+      rgb[c] = up ? v : 0.0;
+    }
+  }
+  // ashikhminshirley.h:98-140
+  __device__ __forceinline__ void spec_sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                              uint32_t& flag) const
+  {
+    BBM_F64_SAMPLE_PROLOGUE
+    double cp, sp, cosT;
+    if (Aniso)
+    {
+      double phi = atan(sqrt((su + 1.0) / (sv + 1.0)) * tan(xi0 * (2.0 * kPi)));
+      phi = ((xi0 > 0.25) && (xi0 < 0.75)) ? phi + kPi : phi;
+      sincos(phi, &sp, &cp);
+      cosT = pow(xi1, 1.0 / ((su * (cp * cp)) + (sv * (sp * sp)) + 1.0));
+    }
+    else
+    {
+      sincos(xi0 * (2.0 * kPi), &sp, &cp);
+      cosT = pow(xi1, 1.0 / (su + 1.0));
+    }
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    dir = reflect(out, mk(cp * sinT, sp * sinT, cosT));
+    pdf = spec_pdf(dir, out, component);
+    flag = kFlagSpecular;
+  }
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    if constexpr (!FULL) { spec_sample(out, xi0, xi1, component, dir, pdf, flag); return; }
+    else {
+    if (!(component & kFlagDiffuse)) { spec_sample(out, xi0, xi1, component, dir, pdf, flag); return; }
+    const double one[3] = {1.0, 1.0, 1.0};
+    const Lambertian lam(one);
+    if (!(component & kFlagSpecular)) { lam.sample(out, xi0, xi1, component, dir, pdf, flag); return; }
+    // ashikhminshirleyfull.h:96-124: one-sample mixture of the specular lobe and cosine sampling
+    const double da = diff_albedo(), sa = fres.hsum();
+    const double dw = da / (da + sa), sw = 1.0 - dw;
+    d3 ds, dd; double ps, pd; uint32_t fs, fd;
+    spec_sample(out, (sw > kEps) ? xi0 / sw : 0.0, xi1, component, ds, ps, fs);
+    lam.sample(out, (dw > kEps) ? (xi0 - sw) / dw : 0.0, xi1, component, dd, pd, fd);
+    const bool pick_s = xi0 <= sw;
+    dir = pick_s ? ds : dd;
+    flag = pick_s ? fs : fd;
+    pdf = sw * ps + dw * pd;
+    }
+  }
+};
+
+// Low et al.'s smooth-surface model (bsdfmodel/lowsmooth.h:17-194): A (RGB), B, C, eta
+struct LowSmooth
+{
+  static constexpr int kParams = 6;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double A[3], B, C;
+  FresnelCook fres;
+  __device__ explicit LowSmooth(const double* p) : B(p[3]), C(p[4]), fres(p + 5) { A[0] = p[0]; A[1] = p[1]; A[2] = p[2]; }
+  // B InvPi / temp (lowsmooth.h:130-135)
+  __device__ __forceinline__ double md(d3 out) const
+  {
+    const double ro2 = sin_theta2(out);
+    const double bb = B * (1.0 - ro2);
+    const double t = 1.0 + (2 * B * (1.0 + ro2)) + bb * bb;
+    const double temp = -log(2.0) + log(1 + B * (1 - ro2) + safe_sqrt(t));
+    return B * kInvPi * (1.0 / temp);
+  }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
+    const double dp2 = sqnorm2(in.x + out.x, in.y + out.y);
+    const double cosD = safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y));
+    const double S = pow(1.0 + B * dp2, -C);
+    const double Q = fres.eval(cosD);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0;
+    pdf = active ? md(out) / (1.0 + B * dp2) * in.z : 0.0;
+  }
+  // lowsmooth.h:166-176
+  __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    const double factor = (fabs(C - 1) < kEps) ? log(B + 1) / (2 * B) : (1.0 - pow(B + 1, 1 - C)) / (2 * B * (C - 1));
+    const double q = (fres.eta - 1) / (fres.eta + 1);
+    const double R0 = q * q;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? ((2.0 * kPi * A[c]) * factor) * R0 : 0.0;
+  }
+  // lowsmooth.h:75-111
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    BBM_F64_SAMPLE_PROLOGUE
+    const double ro2 = sin_theta2(out);
+    const double bb = B * (1 - ro2);
+    double temp = 1.0 + (2 * B * (1.0 + ro2)) + bb * bb;
+    temp = -log(2.0) + log(1 + B * (1 - ro2) + safe_sqrt(temp));
+    const double mdpi = B * (1.0 / temp);
+    const double E = 2.0 * exp(xi0 * B * (1.0 / mdpi));
+    const double ri = safe_sqrt((E - 2) * (E + 2 * B * ro2) / (2 * E * B));
+    const double ro = sqrt(ro2);
+    const double rp = ri + ro, rm = ri - ro;
+    const double scale = sqrt((1.0 + B * (rp * rp)) / (1.0 + B * (rm * rm)));
+    double phio = atan2(out.y, out.x);
+    phio = (phio < 0) ? phio + 2.0 * kPi : phio;
+    const double phi = 2.0 * atan(tan(xi1 * kPi) * scale) + phio;
+    double sp, cp;
+    sincos(phi, &sp, &cp);
+    dir = mk(cp * ri, sp * ri, safe_sqrt(1.0 - ri * ri));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+#undef BBM_F64_SAMPLE_PROLOGUE
 
 // Compositions (the floatRGB registry's, models.hpp)
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;
@@ -410,6 +977,24 @@ using AggCookTorranceM = Aggregate<Lambertian, CookTorranceM>;
 using AggGGXM = Aggregate<Lambertian, GGXM>;
 using AggNganCookTorranceM = Aggregate<Lambertian, NganCookTorranceM>;
 using AggLowMicrofacetM = Aggregate<Lambertian, LowMicrofacetM>;
+using WardM = Ward<0, true>;
+using WardDuerM = Ward<1, true>;
+using WardDGMM = Ward<2, true>;
+using NganWardM = Ward<0, false>;
+using NganWardDuerM = Ward<1, false>;
+using LafortuneM = Lafortune<true, false>;
+using NganLafortuneM = Lafortune<false, true>;
+using ASM = AshikhminShirley<FresnelSchlickRGB, true, false, false>;
+using ASFullM = AshikhminShirley<FresnelSchlickRGB, true, false, true>;
+using LowASM = AshikhminShirley<ScalarFresnel3<FresnelCook>, false, true, false>;
+using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, false>;
+using AggLowASM = Aggregate<Lambertian, LowASM>;
+using AggLowSmoothM = Aggregate<Lambertian, LowSmooth>;
+using AggNganASM = Aggregate<Lambertian, NganASM>;
+using AggPhongM = Aggregate<Lambertian, PhongLobe>;
+using AggNganLafortuneM = Aggregate<Lambertian, NganLafortuneM>;
+using AggNganWardM = Aggregate<Lambertian, NganWardM>;
+using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 
 // ------------------------------------------------------------------------------------------------- kernels
 
@@ -437,12 +1022,24 @@ struct ReflArgsF64
   ParamBlockF64 p;
 };
 
+struct SampleArgsF64
+{
+  const double* ox; const double* oy; const double* oz;
+  const double* xi0; const double* xi1;
+  const uint8_t* mask;
+  double* dx; double* dy; double* dz; double* pdf; uint32_t* flag;
+  uint64_t n;
+  uint32_t component;
+  ParamBlockF64 p;
+};
+
 using EvalLauncherF64 = int (*)(const EvalArgsF64&, hipStream_t);
 using ReflLauncherF64 = int (*)(const ReflArgsF64&, hipStream_t);
+using SampleLauncherF64 = int (*)(const SampleArgsF64&, hipStream_t);
 
 // A composition's f64 launchers (f64.hip), looked up by registry name; nullptr for a model without a doubleRGB
 // kernel.
-struct F64Launchers { EvalLauncherF64 eval_pdf; ReflLauncherF64 reflectance; };
+struct F64Launchers { EvalLauncherF64 eval_pdf; ReflLauncherF64 reflectance; SampleLauncherF64 sample; };
 const F64Launchers* f64_launchers(const char* name);
 
 }  // namespace f64

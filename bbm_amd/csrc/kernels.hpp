@@ -114,6 +114,11 @@ __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, floa
 // per SIMD (too few to hide the f64 / transcendental latencies).
 template<class Model> struct eval_waves { static constexpr int value = 1; };
 
+// Grid cap of the eval kernels (0 = a full grid, one workgroup per 1024 pairs).  The model is constructed once per
+// thread from the kernarg parameters; where that constructor is expensive (the Student-T NDF's two tgamma and a pow
+// per thread) a capped grid-stride launch amortises it over several iterations.
+template<class Model> struct eval_grid_cap { static constexpr uint64_t value = 0; };
+
 template<class Model, int MODE, bool MASK, bool NT>
 __global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_waves_per_eu(eval_waves<Model>::value, 8)))
 void k_eval_pdf_v4(EvalArgs a)
@@ -552,6 +557,7 @@ int launch_mode(const EvalArgs& a0, hipStream_t s)
   uint64_t blocks = (units + per_block - 1) / per_block;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
+  if (eval_grid_cap<Model>::value && blocks > eval_grid_cap<Model>::value) blocks = eval_grid_cap<Model>::value;
 #ifdef BBM_HIP_EXPERIMENTAL
   if (vec && pairs_per_thread() == 8)
     hipLaunchKernelGGL((k_eval_pdf_v8<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);

@@ -21,6 +21,7 @@ namespace bbmhip {
 template<class B> struct compact_eval<Aggregate<Lambertian, B>> { static constexpr bool value = compact_eval<B>::value; };
 template<class B> struct eval_waves<Aggregate<Lambertian, B>> { static constexpr int value = eval_waves<B>::value; };
 template<class B> struct loss_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_waves<B>::value; };
+template<class B> struct eval_grid_cap<Aggregate<Lambertian, B>> { static constexpr uint64_t value = eval_grid_cap<B>::value; };
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
 // Bagher's evaluation holds ~180 VGPRs (two waves per SIMD) unconstrained.  Measured (10M pairs, eval+pdf,
@@ -30,6 +31,10 @@ struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { 
 #define BBM_HIP_BAGHER_WAVES 3
 #endif
 template<> struct eval_waves<Bagher> { static constexpr int value = BBM_HIP_BAGHER_WAVES; };
+
+// Ribardiere's per-thread Student-T setup (two tgamma, a pow): 2048 workgroups (8 per CU, each thread ~5 iterations
+// over 10M pairs) measured 0.139 -> 0.121 ms per 10M-pair eval (1024 / 4096 / 8192: 0.125 / 0.128 / 0.134;
+// tools/gpu_ab_blocks.sh); the HBM-bound models lose 5-15 % under the same cap and keep the full grid.
 
 // Compositions (reference file:line):
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;         // bsdfmodel/cooktorrance.h:28-34
@@ -44,6 +49,8 @@ using RibardiereM = Microfacet<StudentT<false>, Uncorrelated, FresnelCook, Norm:
 using RibardiereAnisoM = Microfacet<StudentT<true>, Uncorrelated, FresnelCook, Norm::Walter, true>;              // bsdfmodel/ribardiere.h:46-52
 
 using LowMicrofacetM = Microfacet<LowNdf, VGroove, FresnelCook, Norm::Cook, true>;                             // bsdfmodel/lowmicrofacet.h:37-70, low.h:40-41
+template<> struct eval_grid_cap<RibardiereM> { static constexpr uint64_t value = 2048; };
+template<> struct eval_grid_cap<RibardiereAnisoM> { static constexpr uint64_t value = 2048; };
 using WardM = Ward<0, true>;                  // bsdfmodel/ward.h:26-168
 using WardDuerM = Ward<1, true>;              // bsdfmodel/wardduer.h:29-81
 using WardDGMM = Ward<2, true>;               // bsdfmodel/wardduergeislermoroder.h:29-81

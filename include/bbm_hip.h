@@ -122,14 +122,19 @@ int bbm_hip_reflectance(int model_id, const float* params, int nparams,
 
 /* The reference's doubleRGB configuration (backbone/native/include/backbone.h:41-42: Value = double, Spectrum =
  * color<double>): the same calls on SoA float64 arrays with a double parameter vector, evaluated in f64 on the
- * device.  Available for the models bbm_hip_model_has_f64 reports (Lambertian, OrenNayar, the microfacet
- * compositions and their Aggregate(Lambertian, X) fits); BBM_HIP_ERR_UNSUPPORTED for the others. */
+ * device.  Available for the models bbm_hip_model_has_f64 reports (every analytic model but Bagher, EPD and
+ * the He family, and their Aggregate(Lambertian, X) fits); BBM_HIP_ERR_UNSUPPORTED for the others. */
 int bbm_hip_model_has_f64(int model_id);                /* 1 / 0, <0 for an unknown id */
 int bbm_hip_eval_pdf_f64(int model_id, const double* params, int nparams,
                          const double* in_x, const double* in_y, const double* in_z,
                          const double* out_x, const double* out_y, const double* out_z,
                          const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
                          double* r, double* g, double* b, double* pdf, void* stream);
+int bbm_hip_sample_f64(int model_id, const double* params, int nparams,
+                       const double* out_x, const double* out_y, const double* out_z,
+                       const double* xi0, const double* xi1,
+                       const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                       double* dir_x, double* dir_y, double* dir_z, double* pdf, uint32_t* flag, void* stream);
 int bbm_hip_reflectance_f64(int model_id, const double* params, int nparams,
                             const double* out_x, const double* out_y, const double* out_z,
                             const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,

@@ -70,14 +70,17 @@ struct aggv
          &ops<typename aggv<__VA_ARGS__>::d>::template evalpdf<double>, \
          &ops<typename aggv<__VA_ARGS__>::f>::template sample<float>, \
          &ops<typename aggv<__VA_ARGS__>::f>::template reflectance<float>, \
-         &ops<typename aggv<__VA_ARGS__>::f>::from_string, &ops<typename aggv<__VA_ARGS__>::d>::template reflectance<double> }
+         &ops<typename aggv<__VA_ARGS__>::f>::from_string, &ops<typename aggv<__VA_ARGS__>::d>::template reflectance<double>, \
+         &ops<typename aggv<__VA_ARGS__>::d>::template sample<double>, \
+         &ops<typename aggv<__VA_ARGS__>::d>::template evalpdf<double, double> }
 
 #define BBMREF_AGG(X, KEY) \
   entry{ KEY, \
          &ops<agg<X>>::defaults, &ops<agg<X>>::bounds, &ops<agg<X>>::to_string, \
          &ops<agg<X>>::template evalpdf<float>, &ops<aggd<X>>::template evalpdf<double>, \
          &ops<agg<X>>::template sample<float>, &ops<agg<X>>::template reflectance<float>, &ops<agg<X>>::from_string, \
-         &ops<aggd<X>>::template reflectance<double> }
+         &ops<aggd<X>>::template reflectance<double>, &ops<aggd<X>>::template sample<double>, \
+         &ops<aggd<X>>::template evalpdf<double, double> }
 
 const std::vector<entry>& aggregate_registry()
 {

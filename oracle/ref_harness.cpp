@@ -152,6 +152,27 @@ int bbmref_reflectance(const char* name, const float* p, int np, size_t n,
   return 0;
 }
 
+int bbmref_eval_pdf_dd(const char* name, const float* p, int np, size_t n,
+                       const double* ix, const double* iy, const double* iz,
+                       const double* ox, const double* oy, const double* oz,
+                       uint32_t component, uint32_t unit, int mode,
+                       double* r, double* g, double* b, double* pdf, int nthreads)
+{
+  auto e = find(name); if(!e || !e->evalpdf_dd) return -1;
+  e->evalpdf_dd(p, np, n, ix, iy, iz, ox, oy, oz, component, unit, mode, r, g, b, pdf, nthreads);
+  return 0;
+}
+
+int bbmref_sample_double(const char* name, const float* p, int np, size_t n,
+                         const float* ox, const float* oy, const float* oz, const float* xi0, const float* xi1,
+                         uint32_t component, uint32_t unit,
+                         double* dx, double* dy, double* dz, double* pdf, uint32_t* flag, int nthreads)
+{
+  auto e = find(name); if(!e || !e->sample_d) return -1;
+  e->sample_d(p, np, n, ox, oy, oz, xi0, xi1, component, unit, dx, dy, dz, pdf, flag, nthreads);
+  return 0;
+}
+
 int bbmref_reflectance_double(const char* name, const float* p, int np, size_t n,
                               const float* ox, const float* oy, const float* oz,
                               uint32_t component, uint32_t unit, double* r, double* g, double* b)

@@ -120,10 +120,10 @@ struct ops
   }
 
   // mode bit 1 = eval, bit 2 = pdf
-  template<typename OUT>
+  template<typename OUT, typename IN = float>
   static void evalpdf(const float* p, int np, size_t n,
-                      const float* ix, const float* iy, const float* iz,
-                      const float* ox, const float* oy, const float* oz,
+                      const IN* ix, const IN* iy, const IN* iz,
+                      const IN* ox, const IN* oy, const IN* oz,
                       uint32_t component, uint32_t unit, int mode,
                       OUT* r, OUT* g, OUT* b, OUT* pdf, int nthreads)
   {
@@ -209,6 +209,9 @@ struct entry
   void (*reflectance_f)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, float*, float*, float*);
   int (*from_string)(const char*, float*, int) = nullptr;
   void (*reflectance_d)(const float*, int, size_t, const float*, const float*, const float*, uint32_t, uint32_t, double*, double*, double*) = nullptr;
+  void (*sample_d)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, double*, double*, double*, double*, uint32_t*, int) = nullptr;
+  // doubleRGB eval / pdf at double directions (the per-lane proofs of the f64 kernels perturb directions in double)
+  void (*evalpdf_dd)(const float*, int, size_t, const double*, const double*, const double*, const double*, const double*, const double*, uint32_t, uint32_t, int, double*, double*, double*, double*, int) = nullptr;
 };
 
 #define BBMREF_ENTRY(MODEL) BBMREF_ENTRY_NS(bbm, MODEL)
@@ -222,7 +225,9 @@ struct entry
          &ops<NS::MODEL<bbm::floatRGB>>::template sample<float>, \
          &ops<NS::MODEL<bbm::floatRGB>>::template reflectance<float>, \
          &ops<NS::MODEL<bbm::floatRGB>>::from_string, \
-         &ops<NS::MODEL<bbm::doubleRGB>>::template reflectance<double> }
+         &ops<NS::MODEL<bbm::doubleRGB>>::template reflectance<double>, \
+         &ops<NS::MODEL<bbm::doubleRGB>>::template sample<double>, \
+         &ops<NS::MODEL<bbm::doubleRGB>>::template evalpdf<double, double> }
 
 
 } // namespace bbmref

@@ -485,16 +485,28 @@ static bool check_model_f64(const MODEL& model, size_t n, unsigned seed)
       const double s = std::sqrt(std::max(1.0 - z * z, 0.0));
       h[3 * k + 0][i] = s * std::cos(phi); h[3 * k + 1][i] = s * std::sin(phi); h[3 * k + 2][i] = z;
     }
-  std::vector<double*> d(13, nullptr);   // in xyz, out xyz, eval rgb, pdf, reflectance rgb
+  std::vector<double> xi[2];
+  for(auto& v : xi) { v.resize(n); for(auto& x : v) x = u(rng); }
+  // in xyz, out xyz, eval rgb, pdf, reflectance rgb, xi0, xi1, sample direction xyz, sample pdf
+  std::vector<double*> d(19, nullptr);
   for(auto& p : d) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(double)));
+  uint32_t* dflag = nullptr;
+  HIPCHECK(hipMalloc(reinterpret_cast<void**>(&dflag), n * sizeof(uint32_t)));
   for(int k = 0; k < 6; ++k) HIPCHECK(hipMemcpy(d[size_t(k)], h[k].data(), n * sizeof(double), hipMemcpyHostToDevice));
+  for(int k = 0; k < 2; ++k) HIPCHECK(hipMemcpy(d[size_t(13 + k)], xi[k].data(), n * sizeof(double), hipMemcpyHostToDevice));
   bbm::hip::eval_pdf(model, bbm::hip::soa3d{d[0], d[1], d[2]}, bbm::hip::soa3d{d[3], d[4], d[5]}, n,
                      bbm::hip::soa3d_out{d[6], d[7], d[8]}, d[9]);
   bbm::hip::reflectance(model, bbm::hip::soa3d{d[3], d[4], d[5]}, n, bbm::hip::soa3d_out{d[10], d[11], d[12]});
-  std::vector<double> g[4], rf[3];
+  bbm::hip::sample(model, bbm::hip::soa3d{d[3], d[4], d[5]}, d[13], d[14], n, bbm::hip::soa3d_out{d[15], d[16], d[17]},
+                   d[18], dflag);
+  std::vector<double> g[4], rf[3], sd[4];
+  std::vector<uint32_t> sf(n);
   for(int k = 0; k < 4; ++k) { g[k].resize(n); HIPCHECK(hipMemcpy(g[k].data(), d[size_t(6 + k)], n * sizeof(double), hipMemcpyDeviceToHost)); }
   for(int k = 0; k < 3; ++k) { rf[k].resize(n); HIPCHECK(hipMemcpy(rf[k].data(), d[size_t(10 + k)], n * sizeof(double), hipMemcpyDeviceToHost)); }
+  for(int k = 0; k < 4; ++k) { sd[k].resize(n); HIPCHECK(hipMemcpy(sd[k].data(), d[size_t(15 + k)], n * sizeof(double), hipMemcpyDeviceToHost)); }
+  HIPCHECK(hipMemcpy(sf.data(), dflag, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   for(auto& p : d) (void)hipFree(p);
+  (void)hipFree(dflag);
   size_t bad = 0;
   double worst = 0;
   auto lane = [&](double got, double want) {
@@ -510,6 +522,10 @@ static bool check_model_f64(const MODEL& model, size_t n, unsigned seed)
     const auto r = model.reflectance(vout);
     for(int c = 0; c < 3; ++c) { lane(g[c][i], double(e[c])); lane(rf[c][i], double(r[c])); }
     lane(g[3][i], double(model.pdf(vin, vout)));
+    const auto smp = model.sample(vout, typename MODEL::Vec2d(xi[0][i], xi[1][i]));
+    if(uint32_t(smp.flag) != sf[i]) ++bad;
+    for(int c = 0; c < 3; ++c) if(std::fabs(sd[c][i] - double(smp.direction[c])) > 1e-5) ++bad;
+    lane(sd[3][i], double(smp.pdf));
   }
   const bool ok = bad == 0 && worst <= 1e-10;
   std::printf("{\"model\": \"%s\", \"config\": \"doubleRGB\", \"n\": %zu, \"violations\": %zu, \"max_rel_normal\": %.3e, \"ok\": %s}\n",
@@ -608,6 +624,11 @@ int main()
   CHECK_D(bbm::ribardiereanisotropic<D>) CHECK_D(bbm::lowmicrofacet<D>) CHECK_D(bbm::lowmicrofacetfit<D>)
   CHECK_D(bbm::aggregatemodel<bbm::lambertian<D>, bbm::cooktorrance<D>>)
   CHECK_D(bbm::aggregatemodel<bbm::lambertian<D>, bbm::ngancooktorrance<D>>)
+  CHECK_D(bbm::ward<D>) CHECK_D(bbm::wardduer<D>) CHECK_D(bbm::wardduergeislermoroder<D>) CHECK_D(bbm::nganward<D>)
+  CHECK_D(bbm::nganwardduer<D>) CHECK_D(bbm::phong<D>) CHECK_D(bbm::nganblinnphong<D>) CHECK_D(bbm::lafortune<D>)
+  CHECK_D(bbm::nganlafortune<D>) CHECK_D(bbm::ashikhminshirley<D>) CHECK_D(bbm::ashikhminshirleyfull<D>)
+  CHECK_D(bbm::lowashikhminshirley<D>) CHECK_D(bbm::nganashikhminshirley<D>) CHECK_D(bbm::lowsmooth<D>)
+  CHECK_D(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>)
 #undef CHECK_D
   {
     // attributes that are not floats reach the kernel unrounded

@@ -205,7 +205,11 @@ int main()
   F64(bbm::cooktorrancewalter<D>) F64(bbm::cooktorranceheitz<D>) F64(bbm::ggxheitz<D>) F64(bbm::ngancooktorrance<D>)
   F64(bbm::phongwalter<D>) F64(bbm::ribardiere<D>) F64(bbm::ribardiereanisotropic<D>) F64(bbm::lowmicrofacet<D>)
   F64(bbm::lowmicrofacetfit<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::cooktorrance<D>>)
-  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::ggx<D>>)
+  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::ggx<D>>) F64(bbm::ward<D>) F64(bbm::wardduer<D>)
+  F64(bbm::wardduergeislermoroder<D>) F64(bbm::nganward<D>) F64(bbm::nganwardduer<D>) F64(bbm::phong<D>)
+  F64(bbm::nganblinnphong<D>) F64(bbm::lafortune<D>) F64(bbm::nganlafortune<D>) F64(bbm::ashikhminshirley<D>)
+  F64(bbm::ashikhminshirleyfull<D>) F64(bbm::lowashikhminshirley<D>) F64(bbm::nganashikhminshirley<D>)
+  F64(bbm::lowsmooth<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>)
 #undef F64
 
   // an unknown model string fails loudly with the library's error

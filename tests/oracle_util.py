@@ -133,6 +133,39 @@ def ref_eval_pdf_double(name, params, din, dout, component=3, unit=0, nthreads=1
     return res
 
 
+def ref_eval_pdf_dd(name, params, din, dout, component=3, unit=0, nthreads=1):
+    """(4, N) float64: the reference's doubleRGB eval + pdf at float64 directions."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    din = np.ascontiguousarray(din, dtype=np.float64)
+    dout = np.ascontiguousarray(dout, dtype=np.float64)
+    n = din.shape[1]
+    res = np.zeros((4, n), np.float64)
+    rc = lib.bbmref_eval_pdf_dd(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(din[0]), _fp(din[1]),
+                                _fp(din[2]), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component),
+                                ctypes.c_uint32(unit), 3, _fp(res[0]), _fp(res[1]), _fp(res[2]), _fp(res[3]), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return res
+
+
+def ref_sample_double(name, params, dout, xi, component=3, unit=0, nthreads=1):
+    """doubleRGB sample(out, xi) from the reference: ((3, N) float64 direction, (N,) float64 pdf, (N,) flags)."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    xi = np.ascontiguousarray(xi, dtype=np.float32)
+    n = dout.shape[1]
+    d = np.zeros((4, n), np.float64)
+    flag = np.zeros(n, np.uint32)
+    rc = lib.bbmref_sample_double(name.encode(), _fp(params), params.size, ctypes.c_size_t(n), _fp(dout[0]),
+                                  _fp(dout[1]), _fp(dout[2]), _fp(xi[0]), _fp(xi[1]), ctypes.c_uint32(component),
+                                  ctypes.c_uint32(unit), _fp(d[0]), _fp(d[1]), _fp(d[2]), _fp(d[3]), _fp(flag), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle has no model {name} (rc={rc})")
+    return d[:3], d[3], flag
+
+
 def ref_reflectance_double(name, params, dout, component=3, unit=0):
     """(3, N) float64: reflectance(out) from the reference's doubleRGB configuration."""
     lib = ref()

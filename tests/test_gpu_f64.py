@@ -5,7 +5,8 @@ Checked through the C-ABI on
   * the golden direction set, against the doubleRGB outputs the reference wrote into tests/golden (evalpdf_double);
   * fresh seeded batches of 1M pairs per model and parameter set, against the reference itself (oracle/_ref,
     bbmref_eval_pdf_double), hemisphere and sphere inputs;
-  * reflectance per component, against bbmref_reflectance_double.
+  * reflectance per component, against bbmref_reflectance_double;
+  * sample(out, xi) -- direction, pdf, flag -- against bbmref_sample_double.
 The bar is north_star's, per lane: |gpu - ref| <= 1e-5 |ref| (tests/oracle_util.parity_ok_f64); every lane outside
 it must be proven by the input-ulps argument of test_gpu_parity.py.  The statistics (max relative error, bit-exact
 fraction) go to gpurun_out/parity_f64_*.json: in double the device's and glibc's exp / pow / tgamma differ by an
@@ -77,11 +78,14 @@ def _check(got, ref, what, ref_fn=None, inputs=None):
             "frac_bit_exact": float(np.mean(got == ref)), "proven_input_ulps": proven}
 
 
-def test_f64_models_cover_the_microfacet_family(bbm):
+def test_f64_models_cover_the_analytic_families(bbm):
     names = set(_f64_models(bbm))
     for want in ("Lambertian", "OrenNayar", "CookTorrance", "GGX", "CookTorranceWalter", "CookTorranceHeitz",
                  "GGXHeitz", "NganCookTorrance", "PhongWalter", "Ribardiere", "RibardiereAnisotropic",
-                 "LowMicrofacet", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,GGX>"):
+                 "LowMicrofacet", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,GGX>", "Ward",
+                 "WardDuer", "WardDuerGeislerMoroder", "NganWard", "NganWardDuer", "Phong", "NganBlinnPhong",
+                 "Lafortune", "NganLafortune", "AshikhminShirley", "AshikhminShirleyFull", "LowAshikhminShirley",
+                 "NganAshikhminShirley", "LowSmooth", "Aggregate<Lambertian,NganWardDuer>"):
         assert want in names, want
 
 
@@ -142,6 +146,89 @@ def test_f64_reflectance(bbm):
                 ref = ou.ref_reflectance_double(name, g[f"params{si}"], INP["sout"], comp)
                 stats[f"{name}[{si}]/{comp}"] = _check(got, ref, f"{name}[{si}] f64 reflectance/{comp}")
     _report("reflectance", stats)
+
+
+def _pdf_at_direction_proof(name, params, d_gpu, dout, p_gpu, k=4, trials=64, seed=5):
+    """Per-lane proof for a sample pdf outside the bar: the reference's doubleRGB pdf at the GPU's sampled direction,
+    moved by <= k double ulps per coordinate, brackets the GPU pdf -- the lane's pdf is ill-conditioned in its
+    direction (e.g. a direction on the equator of a Lafortune lobe, cos^s of a rounding residue)."""
+    n = d_gpu.shape[1]
+    if n == 0:
+        return np.zeros(0, bool)
+    rng = np.random.default_rng(seed)
+    lo = np.full(n, np.inf)
+    hi = np.full(n, -np.inf)
+    out = np.asarray(dout, np.float32).astype(np.float64)
+    for t in range(trials + 1):
+        steps = np.zeros((3, n), np.int64) if t == 0 else rng.integers(-k, k + 1, (3, n))
+        d = d_gpu.copy()
+        for _ in range(k):
+            move = steps != 0
+            d = np.where(move, np.nextafter(d, np.where(steps > 0, np.inf, -np.inf)), d)
+            steps = steps - np.sign(steps)
+        p = ou.ref_eval_pdf_dd(name, params, d, out, nthreads=8)[3]
+        lo, hi = np.minimum(lo, p), np.maximum(hi, p)
+    return (lo <= p_gpu) & (p_gpu <= hi) | ou.parity_ok_f64(p_gpu, lo) | ou.parity_ok_f64(p_gpu, hi)
+
+
+def _xi_ulps_proof(name, params, dout, xi, d_gpu, f_gpu, k=2):
+    """Per-lane proof for a sample whose flag or direction differs from the reference's: the reference, given xi moved
+    by <= k float steps per coordinate, returns the GPU's flag and a direction within 1e-5 -- the lane sits on a
+    decision boundary of the sampler (e.g. xi0 = 1 picks the last child of an aggregate only if
+    xi0 sum - w_0 <= w_1 survives the rounding of the children's reflectance weights, an ulp of pow apart)."""
+    n = xi.shape[1]
+    ok = np.zeros(n, bool)
+    if n == 0:
+        return ok
+    for s0 in range(-k, k + 1):
+        for s1 in range(-k, k + 1):
+            x = np.asarray(xi, np.float32).copy()
+            for row, st in ((0, s0), (1, s1)):
+                for _ in range(abs(st)):
+                    x[row] = np.nextafter(x[row], np.float32(np.inf if st > 0 else -np.inf))
+            x = np.clip(x, 0, 1).astype(np.float32)
+            d, _, f = ou.ref_sample_double(name, params, dout, x, nthreads=8)
+            ok |= (f == f_gpu.astype(np.uint32)) & (np.abs(d - d_gpu).max(0) <= 1e-5)
+    return ok
+
+
+@pytest.mark.parametrize("mode_out", [0, 1])
+def test_f64_sample(bbm, mode_out):
+    """sample(out, xi) in doubleRGB: flags identical, every direction component within 1e-5 (measured ~1e-13: the
+    VNDF inversions run the same f64 arithmetic, erf / exp / log differ by an ulp), pdf at the 1e-5 bar per lane."""
+    n = 1 << 18
+    dout = bbm.fill_directions(0x5A3, 1, 0, n, mode=mode_out).cpu().numpy()
+    xi = np.random.default_rng(17).random((2, n), dtype=np.float32)
+    xi[:, :7] = [[0, 1, 0, 1, 0.5, 1e-7, 0.9999999], [0, 0, 1, 1, 0.5, 0.9999999, 1e-7]]
+    stats = {}
+    for name in _f64_models(bbm):
+        g = ou.golden_model(name)
+        for si in (0, 2):
+            m = bbm.BsdfModel(name)
+            m.set_parameter_values(g[f"params{si}"])
+            s = m.sample(_d(dout), _d(xi))
+            torch.cuda.synchronize()
+            d_gpu, p_gpu, f_gpu = s.direction.cpu().numpy(), s.pdf.cpu().numpy(), s.flag.cpu().numpy()
+            d_ref, p_ref, f_ref = ou.ref_sample_double(name, g[f"params{si}"], dout, xi, nthreads=8)
+            what = f"{name}[{si}] f64 sample {mode_out}"
+            derr = np.abs(d_gpu - d_ref).max(0)
+            off = np.nonzero((f_gpu.astype(np.uint32) != f_ref) | (derr > 1e-5))[0]
+            by_xi = _xi_ulps_proof(name, g[f"params{si}"], dout[:, off], xi[:, off], d_gpu[:, off], f_gpu[off])
+            assert by_xi.all(), (f"{what}: {int((~by_xi).sum())} samples off (flag / direction); lanes {off[~by_xi][:4]} "
+                                 f"got {d_gpu[:, off[~by_xi][:4]].T} {f_gpu[off[~by_xi][:4]]} ref {d_ref[:, off[~by_xi][:4]].T} "
+                                 f"{f_ref[off[~by_xi][:4]]}")
+            # the proven lanes' pdfs are those of the GPU's own direction (checked by the pdf-at-direction proof)
+            d_ref[:, off], p_ref[off] = d_gpu[:, off], np.nan
+            derr = np.abs(d_gpu - d_ref).max(0)
+            ok = ou.parity_ok_f64(p_gpu, p_ref)
+            bad = np.nonzero(~ok)[0]
+            proven = _pdf_at_direction_proof(name, g[f"params{si}"], d_gpu[:, bad], dout[:, bad], p_gpu[bad])
+            assert proven.all(), f"{what}: pdf lanes {bad[~proven][:4]} got {p_gpu[bad[~proven][:4]]} ref {p_ref[bad[~proven][:4]]}"
+            stats[f"{name}[{si}]"] = {"n": n, "max_dir_abs_err": float(derr.max()), "pdf_proven_at_direction": int(bad.size),
+                                      "sample_proven_xi_ulps": int(off.size),
+                                      "max_pdf_rel_in_bar": float(ou.rel_err_f64(p_gpu[ok], p_ref[ok]).max(initial=0)),
+                                      "frac_dir_bit_exact": float(np.mean((d_gpu == d_ref).all(0)))}
+    _report(f"sample_{mode_out}", stats)
 
 
 def test_f64_mask_unaligned_and_odd_sizes(bbm):

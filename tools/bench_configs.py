@@ -249,8 +249,9 @@ def bench_f64(args, dist, rank, world):
         graph = _graph(lambda s: mm.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=s), GRAPH_REPS)
         _, step_ms = _timed(graph.replay, args, dist, stream)
         k = step_ms / GRAPH_REPS
-        per[name] = {"kernel_ms": k, "pairs_per_s": m10 / (k * 1e-3), "GB_s": bpp * m10 / (k * 1e-3) / 1e9,
-                     "roofline_frac": bpp * m10 / (k * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        b = 48 if name in Z_ONLY else bpp    # Lambertian reads only z: 16 B in + 32 B out
+        per[name] = {"kernel_ms": k, "pairs_per_s": m10 / (k * 1e-3), "GB_s": b * m10 / (k * 1e-3) / 1e9,
+                     "roofline_frac": b * m10 / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_pair": b}
     if rank == 0:
         global_pairs = n * world if args.scaling == "weak" else args.pairs
         d = {"metric": f"BSDF evals/s (eval+pdf), {args.model}, doubleRGB (f64)", "value": global_pairs * args.steps / elapsed,
