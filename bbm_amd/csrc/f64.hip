@@ -192,6 +192,8 @@ const Entry kF64[] = {
   BBM_HIP_F64("Aggregate<Lambertian,NganLafortune>", AggNganLafortuneM),
   BBM_HIP_F64("Aggregate<Lambertian,NganWard>", AggNganWardM),
   BBM_HIP_F64("Aggregate<Lambertian,NganWardDuer>", AggNganWardDuerM),
+  BBM_HIP_F64("Bagher", Bagher),
+  BBM_HIP_F64("Aggregate<Lambertian,Bagher>", AggBagherM),
 };
 #undef BBM_HIP_F64
 
@@ -201,7 +203,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8 && WardM::kParams == 5 &&
               NganWardM::kParams == 4 && PhongLobe::kParams == 4 && LafortuneM::kParams == 7 &&
               NganLafortuneM::kParams == 6 && ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 &&
-              NganASM::kParams == 5 && LowSmooth::kParams == 6, "f64 nparams must match the floatRGB registry");
+              NganASM::kParams == 5 && LowSmooth::kParams == 6 && Bagher::kParams == 30, "f64 nparams must match the floatRGB registry");
 
 }  // namespace
 

@@ -9,8 +9,8 @@
 //
 // Covered compositions: Lambertian, OrenNayar, every microfacet<NDF, G, F, N> composition of the floatRGB
 // registry (Beckmann / GGX / Phong / Student-T / Low NDFs x v-groove / uncorrelated / height-correlated x Cook /
-// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth) and the
-// Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
+// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth), Bagher and
+// the Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
 // thread with 16 B loads: 48 B in + 32 B out = 80 B per eval+pdf pair.
 #pragma once
 #include "math.hpp"
@@ -962,6 +962,85 @@ struct LowSmooth
 };
 #undef BBM_F64_SAMPLE_PROLOGUE
 
+// --------------------------------------------------------------------------------------------------- Bagher
+
+// spherical::theta(v) (core/spherical.h:26-32): 2 asin(0.5 |v - (0, 0, sign z)|), Pi - that below the horizon
+__device__ __forceinline__ double theta_of(d3 v)
+{
+  const double dz = v.z - copysign(1.0, v.z);
+  const double t = 2.0 * asin(0.5 * sqrt(((0.0 + v.x * v.x) + v.y * v.y) + dz * dz));
+  return (v.z >= 0) ? t : kPi - t;
+}
+
+// scaledmodel<microfacet<ndf::sgd, uncorrelated, fresnel::bagher, Cook>> (bsdfmodel/bagher.h:62-68; ndf/sgd.h:48-63,
+// 143-193): Spectrum-valued NDF / G1 / Fresnel; sampled and pdf'd by GGX with the channel-averaged alpha
+// (sgd.h:73-93).  Parameters as the floatRGB Bagher (spectral.hpp).
+struct Bagher
+{
+  static constexpr int kParams = 30;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3];
+  GGX<false> ggx;
+  __device__ explicit Bagher(const double* q) : ggx(q + 18)
+  {
+    for (int j = 0; j < 3; ++j)
+    {
+      albedo[j] = q[j]; K[j] = q[3 + j]; Lambda[j] = q[6 + j]; c[j] = q[9 + j]; theta0[j] = q[12 + j];
+      k[j] = q[15 + j]; alpha[j] = q[18 + j]; p[j] = q[21 + j]; F0[j] = q[24 + j]; F1[j] = q[27 + j];
+    }
+    ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
+  }
+  __device__ __forceinline__ double G1(int j, double th) const
+  {
+    return (th > theta0[j]) ? 1.0 + Lambda[j] * (1.0 - exp(c[j] * pow(th - theta0[j], k[j]))) : 1.0;
+  }
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
+    const double inh = dot(in, h), outh = dot(out, h);
+    const double tan2 = tan_theta2(h);
+    const double z2 = h.z * h.z;
+    const double dnorm = kPi * (z2 * z2);
+    const bool gmask = (inh > 0) && (outh > 0);
+    const double th_in = theta_of(in), th_out = theta_of(out);
+    const double cosF = 0.5 * (inh + outh);
+    const double x5 = pow(1.0 - cosF, 5.0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+    {
+      const double t = alpha[j] + tan2 / alpha[j];
+      const double den = pow(t, p[j]);
+      const double P22 = (den > kEps) ? exp(-t) / den : 0.0;
+      const double Dj = ((h.z > 0) ? P22 / dnorm : 0.0) * K[j];
+      const double Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0;
+      const double Fj = (F0[j] + (1.0 - F0[j]) * x5) - F1[j] * cosF;
+      const double res = Dj * Gj * Fj / kPi / (in.z * out.z);
+      rgb[j] = active ? res * albedo[j] : 0.0;
+    }
+    pdf = active ? vndf_pdf(ggx, out, h, ggx.eval(h)) / (4.0 * fabs(outh)) : 0.0;
+  }
+  __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    const double x5 = pow(1.0 - out.z, 5.0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rgb[j] = m ? ((F0[j] + (1.0 - F0[j]) * x5) - F1[j] * out.z) / kPi * 4.0 * albedo[j] : 0.0;
+  }
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk(0.0, 0.0, 0.0);
+    pdf = 0.0;
+    flag = kFlagNone;
+    if (!(component & kFlagSpecular) || !xi_ok(xi0, xi1) || !(out.z > 0)) return;
+    dir = reflect(out, ggx.sample(out, xi0, xi1));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = kFlagSpecular;
+  }
+};
+
 // Compositions (the floatRGB registry's, models.hpp)
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;
@@ -995,6 +1074,7 @@ using AggPhongM = Aggregate<Lambertian, PhongLobe>;
 using AggNganLafortuneM = Aggregate<Lambertian, NganLafortuneM>;
 using AggNganWardM = Aggregate<Lambertian, NganWardM>;
 using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
+using AggBagherM = Aggregate<Lambertian, Bagher>;
 
 // ------------------------------------------------------------------------------------------------- kernels
 

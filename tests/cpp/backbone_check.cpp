@@ -209,7 +209,8 @@ int main()
   F64(bbm::wardduergeislermoroder<D>) F64(bbm::nganward<D>) F64(bbm::nganwardduer<D>) F64(bbm::phong<D>)
   F64(bbm::nganblinnphong<D>) F64(bbm::lafortune<D>) F64(bbm::nganlafortune<D>) F64(bbm::ashikhminshirley<D>)
   F64(bbm::ashikhminshirleyfull<D>) F64(bbm::lowashikhminshirley<D>) F64(bbm::nganashikhminshirley<D>)
-  F64(bbm::lowsmooth<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>)
+  F64(bbm::lowsmooth<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>) F64(bbm::bagher<D>)
+  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::bagher<D>>)
 #undef F64
 
   // an unknown model string fails loudly with the library's error

@@ -53,9 +53,10 @@ def test_f64_registry(lib):
     for name in ("Lambertian", "OrenNayar", "CookTorrance", "GGX", "CookTorranceHeitz", "Ribardiere",
                  "LowMicrofacetFit", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,NganCookTorrance>"):
         assert has[name] == 1, name
-    for name in ("Ward", "AshikhminShirleyFull", "LowSmooth", "Aggregate<Lambertian,NganWard>"):
+    for name in ("Ward", "AshikhminShirleyFull", "LowSmooth", "Aggregate<Lambertian,NganWard>", "Bagher",
+                 "Aggregate<Lambertian,Bagher>"):
         assert has[name] == 1, name
-    for name in ("HeWestin", "EPD", "Bagher", "Merl", "Aggregate<Lambertian,Bagher>"):
+    for name in ("HeWestin", "EPD", "Merl", "Aggregate<Lambertian,NganHe>"):
         assert has[name] == 0, name
     assert lib.bbm_hip_model_has_f64(10_000) == -1
     # a model without doubleRGB kernels is refused before anything is launched

@@ -26,6 +26,9 @@ pytestmark = pytest.mark.gpu
 META = ou.golden_meta()
 INP = ou.golden_inputs()
 TIGHT = 1e-10
+# Bagher's shadowing 1 + Lambda (1 - exp(c pow(theta - theta0, k))) cancels twice for published fits (c ~ 1e-7,
+# k ~ 48, G ~ 5e-4): an ulp of pow between ocml and glibc reaches the result amplified ~1e7 (measured 1.2e-9)
+TIGHT_MODEL = {"Bagher": 1e-7, "Aggregate<Lambertian,Bagher>": 1e-7}
 
 
 @pytest.fixture(scope="module")
@@ -58,6 +61,7 @@ def _report(tag, stats):
 
 
 def _check(got, ref, what, ref_fn=None, inputs=None):
+    tight = TIGHT_MODEL.get(what.split("[")[0].split(" ")[0].split("/")[0], TIGHT)
     n = got.shape[-1]
     ok = ou.parity_ok_f64(got, ref).reshape(-1, n).all(0)
     bad = np.nonzero(~ok)[0]
@@ -72,7 +76,7 @@ def _check(got, ref, what, ref_fn=None, inputs=None):
     normal = np.abs(ref) >= ou.DBL_MIN
     # beyond the contract: f64 agrees to ~1e-13 (measured max 8.5e-14 over 65 x 2 M-pair batches); 1e-10 leaves
     # room for ill-conditioned lanes without hiding a real formula difference (those show up at >= 1e-8)
-    assert proven or not normal.any() or err[normal].max() <= TIGHT, f"{what}: max relative error {err[normal].max():.3e}"
+    assert proven or not normal.any() or err[normal].max() <= tight, f"{what}: max relative error {err[normal].max():.3e}"
     return {"lanes": int(n), "max_rel_normal": float(err[normal].max()) if normal.any() else 0.0,
             "frac_lanes_rel_le_1e-12": float(np.mean((err <= 1e-12).reshape(-1, n).all(0))),
             "frac_bit_exact": float(np.mean(got == ref)), "proven_input_ulps": proven}
@@ -85,7 +89,8 @@ def test_f64_models_cover_the_analytic_families(bbm):
                  "LowMicrofacet", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,GGX>", "Ward",
                  "WardDuer", "WardDuerGeislerMoroder", "NganWard", "NganWardDuer", "Phong", "NganBlinnPhong",
                  "Lafortune", "NganLafortune", "AshikhminShirley", "AshikhminShirleyFull", "LowAshikhminShirley",
-                 "NganAshikhminShirley", "LowSmooth", "Aggregate<Lambertian,NganWardDuer>"):
+                 "NganAshikhminShirley", "LowSmooth", "Aggregate<Lambertian,NganWardDuer>", "Bagher",
+                 "Aggregate<Lambertian,Bagher>"):
         assert want in names, want
 
 
