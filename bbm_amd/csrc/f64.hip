@@ -116,9 +116,24 @@ template<class Model> struct grid_cap { static constexpr unsigned value = 0; };
 template<> struct grid_cap<RibardiereM> { static constexpr unsigned value = 2048; };
 template<> struct grid_cap<RibardiereAnisoM> { static constexpr unsigned value = 2048; };
 
-template<class Model>
-int launch_eval_pdf(const EvalArgsF64& a, hipStream_t s)
+// Per-model host work before a launch: EPD's table address into its parameter slot (EpdNdf::kTableSlot)
+template<class Model> struct host_params { static int run(ParamBlockF64&, hipStream_t) { return 0; } };
+template<> struct host_params<EpdM>
 {
+  static int run(ParamBlockF64& p, hipStream_t s)
+  {
+    const float* t = epd_table_device(s);
+    if (!t) return fail(BBM_HIP_ERR_HIP, "EPD: shadowing table unavailable");
+    p.v[EpdNdf::kTableSlot] = __builtin_bit_cast(double, reinterpret_cast<unsigned long long>(t));
+    return 0;
+  }
+};
+
+template<class Model>
+int launch_eval_pdf(const EvalArgsF64& a0, hipStream_t s)
+{
+  EvalArgsF64 a = a0;
+  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
   const bool v2 = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
                   aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
   unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
@@ -131,16 +146,20 @@ int launch_eval_pdf(const EvalArgsF64& a, hipStream_t s)
 }
 
 template<class Model>
-int launch_reflectance(const ReflArgsF64& a, hipStream_t s)
+int launch_reflectance(const ReflArgsF64& a0, hipStream_t s)
 {
+  ReflArgsF64 a = a0;
+  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
   if (a.mask) hipLaunchKernelGGL((k_reflectance_f64<Model, true>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_reflectance_f64<Model, false>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
   return launched("k_reflectance_f64");
 }
 
 template<class Model>
-int launch_sample(const SampleArgsF64& a, hipStream_t s)
+int launch_sample(const SampleArgsF64& a0, hipStream_t s)
 {
+  SampleArgsF64 a = a0;
+  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
   unsigned blocks = grid(a.n);
   if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
   if (a.mask) hipLaunchKernelGGL((k_sample_f64<Model, true>), dim3(blocks), dim3(kBlock), 0, s, a);
@@ -194,6 +213,7 @@ const Entry kF64[] = {
   BBM_HIP_F64("Aggregate<Lambertian,NganWardDuer>", AggNganWardDuerM),
   BBM_HIP_F64("Bagher", Bagher),
   BBM_HIP_F64("Aggregate<Lambertian,Bagher>", AggBagherM),
+  BBM_HIP_F64("EPD", EpdM),
 };
 #undef BBM_HIP_F64
 
@@ -203,7 +223,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8 && WardM::kParams == 5 &&
               NganWardM::kParams == 4 && PhongLobe::kParams == 4 && LafortuneM::kParams == 7 &&
               NganLafortuneM::kParams == 6 && ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 &&
-              NganASM::kParams == 5 && LowSmooth::kParams == 6 && Bagher::kParams == 30, "f64 nparams must match the floatRGB registry");
+              NganASM::kParams == 5 && LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4, "f64 nparams must match the floatRGB registry");
 
 }  // namespace
 

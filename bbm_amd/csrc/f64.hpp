@@ -9,11 +9,12 @@
 //
 // Covered compositions: Lambertian, OrenNayar, every microfacet<NDF, G, F, N> composition of the floatRGB
 // registry (Beckmann / GGX / Phong / Student-T / Low NDFs x v-groove / uncorrelated / height-correlated x Cook /
-// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth), Bagher and
-// the Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
+// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth), Bagher, EPD
+// and the Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
 // thread with 16 B loads: 48 B in + 32 B out = 80 B per eval+pdf pair.
 #pragma once
 #include "math.hpp"
+#include "epd.hpp"      // gamma_q_inv_d
 
 namespace bbmhip {
 namespace f64 {
@@ -1041,6 +1042,124 @@ struct Bagher
   }
 };
 
+// ------------------------------------------------------------------------------------------------------ EPD
+
+// std::lerp(a, b, t) for doubles (libstdc++ <cmath>, C++20): exact at the ends, monotone
+__device__ __forceinline__ double lerp(double a, double b, double t)
+{
+  if ((a <= 0 && b >= 0) || (a >= 0 && b <= 0)) return t * b + (1 - t) * a;
+  if (t == 1) return b;
+  const double x = a + t * (b - a);
+  return ((t > 1) == (b > a)) ? ((b < x) ? x : b) : ((x < b) ? x : b);
+}
+
+// ndf::epd (ndf/epd.h:43-186) in doubleRGB.  G1 is tab<float, {100, 1000}>::interpolate<double> (core/precompute.h:
+// 126-198) of the shadowing table the library builds on the device (inst_epd.hip, epd.hpp): the float entries are
+// read as they are and interpolated in double.  The table's device address travels in the parameter block's
+// slot after the model's four parameters (bit pattern of a double), filled by the launcher.
+struct EpdNdf
+{
+  static constexpr int kParams = 2;
+  static constexpr int kTableSlot = 4;    // EpdM: ndf at offset 0, unscaled, 2 + 2 parameters
+  double beta, p, normalization, inv_p;
+  const float* tab;
+  __device__ explicit EpdNdf(const double* q) : beta(q[0]), p(q[1])
+  {
+    // compute_normalization (epd.h:160-178)
+    normalization = ((p > kEps) ? (p * kInvPi) * (1.0 / tgamma(1.0 / p)) : 0.0) / (beta * beta);
+    inv_p = 1.0 / p;
+    tab = reinterpret_cast<const float*>(__builtin_bit_cast(unsigned long long, q[kTableSlot]));
+  }
+  // epd.h:56-73
+  __device__ __forceinline__ double eval(d3 h) const
+  {
+    const double c2 = h.z * h.z;
+    const double D = normalization * exp(-pow(((1 - c2) / c2) / (beta * beta), p)) / (c2 * c2);
+    return (h.z > 0) ? D : 0.0;
+  }
+  // G1.h:14-16 index maps, then the bilinear interpolation of the clamped floor / ceil entries
+  __device__ __forceinline__ double lookup(double t) const
+  {
+    const double m0 = 5.0 / p - 1.0;
+    const double m1 = exp(-exp(log(1.0 / t) * 0.05)) * 1000.0 - 1.0;
+    auto at = [&](double i0, double i1) {
+      const int r = int(fmin(fmax(i0, 0.0), 99.0)), c = int(fmin(fmax(i1, 0.0), 999.0));
+      return double(tab[r * 1000 + c]);
+    };
+    const double f0 = floor(m0), c0 = ceil(m0), w0 = m0 - f0;
+    const double f1 = floor(m1), c1 = ceil(m1), w1 = m1 - f1;
+    return lerp(lerp(at(f0, f1), at(f0, c1), w1), lerp(at(c0, f1), at(c0, c1), w1), w0);
+  }
+  // epd.h:140-152
+  __device__ __forceinline__ double G1(d3 v, d3 m) const
+  {
+    const bool mask = (v.z > 0) && (dot(v, m) > 0);
+    return mask ? lookup(tan_theta(v) * beta) : 0.0;
+  }
+  // epd.h:118-134
+  __device__ __forceinline__ double pdf(d3, d3 m, double D) const
+  {
+    const double q = D * m.z;
+    return ((m.z > 0) && (q > 0)) ? q : 0.0;
+  }
+  // epd.h:84-106 (Eq. 49-50): tan^2 = beta^2 gamma_q_inv(1/p, xi1)^(1/p); gamma_q_inv_d (epd.hpp) converges the
+  // Halley iteration of util/invgamma.h:404-414 in double
+  __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
+  {
+    if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
+    double sp, cp;
+    sincos(2.0 * kPi * xi0, &sp, &cp);
+    // xi1 = 1: the reference's gamma_q_inv(a, q = 1) starts its Halley iteration at p = 0, x = 0, where
+    // t = (P - p) / R(a, 0) = 0 / 0 (util/invgamma.h:404-414): its sampled normal is NaN, and so is this one
+    const double g = (xi1 >= 1.0) ? __builtin_nan("") : gamma_q_inv_d(inv_p, xi1);
+    const double tan2 = beta * beta * pow(g, inv_p);
+    const double cosT = 1.0 / sqrt(1.0 + tan2);
+    const double sinT = safe_sqrt(1.0 - cosT * cosT);
+    return mk(cp * sinT, sp * sinT, cosT);
+  }
+};
+
+// spherical::phi (core/spherical.h:42-46)
+__device__ __forceinline__ double phi_of(d3 v)
+{
+  const double r = atan2(v.y, v.x);
+  return (r < 0) ? r + 2.0 * kPi : r;
+}
+
+// maskingshadowing::vanginneken (vanginneken.h:30-71)
+struct VanGinneken
+{
+  template<class NDF>
+  __device__ __forceinline__ static double eval(const NDF& ndf, d3 in, d3 out, d3 m, double inm, double outm)
+  {
+    const double phi = fabs(phi_of(in) - phi_of(out));
+    const double lambda = 4.41 * phi / (4.41 * phi + 1.0);
+    const double gi = ndf.G1(in, m), go = ndf.G1(out, m);
+    const double gio = gi * go;
+    const double denom = fmax(gi, go) + lambda * (fmin(gi, go) - gio);
+    return ((inm > 0) && (outm > 0) && (denom > kEps)) ? gio / denom : 0.0;
+  }
+};
+
+// fresnel::complex<Value> (bbm/fresnel_complex.h:38-63), Shirley 1985 Eqs. 2.4-2.7
+struct FresnelComplex
+{
+  static constexpr int kParams = 2;
+  double n, k;
+  __device__ explicit FresnelComplex(const double* q) : n(q[0]), k(q[1]) {}
+  __device__ __forceinline__ double eval(double c) const
+  {
+    const double c2 = c * c, s2 = 1 - c2, n2 = n * n, k2 = k * k;
+    const double temp = n2 - k2 - s2;
+    const double a2b2 = safe_sqrt(temp * temp + 4 * n2 * k2);
+    const double a = safe_sqrt(0.5 * (a2b2 + temp));
+    const double a2c = 2 * a * c;
+    const double Rs = (a2b2 - a2c + c2) / (a2b2 + a2c + c2);
+    const double Rp = Rs * (c2 * a2b2 - (a2c - s2) * s2) / (c2 * a2b2 + (a2c + s2) * s2);
+    return 0.5 * (Rs + Rp);
+  }
+};
+
 // Compositions (the floatRGB registry's, models.hpp)
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;
@@ -1075,6 +1194,7 @@ using AggNganLafortuneM = Aggregate<Lambertian, NganLafortuneM>;
 using AggNganWardM = Aggregate<Lambertian, NganWardM>;
 using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 using AggBagherM = Aggregate<Lambertian, Bagher>;
+using EpdM = Microfacet<EpdNdf, VanGinneken, FresnelComplex, Norm::Walter, false>;   // holzschuchpacanowski.h:34-42
 
 // ------------------------------------------------------------------------------------------------- kernels
 
@@ -1120,6 +1240,11 @@ using SampleLauncherF64 = int (*)(const SampleArgsF64&, hipStream_t);
 // A composition's f64 launchers (f64.hip), looked up by registry name; nullptr for a model without a doubleRGB
 // kernel.
 struct F64Launchers { EvalLauncherF64 eval_pdf; ReflLauncherF64 reflectance; SampleLauncherF64 sample; };
+
+}  // namespace f64
+// EPD's shadowing table on the current device, built on first use (inst_epd.hip); nullptr on failure
+const float* epd_table_device(hipStream_t s);
+namespace f64 {
 const F64Launchers* f64_launchers(const char* name);
 
 }  // namespace f64

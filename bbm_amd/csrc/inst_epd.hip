@@ -173,6 +173,16 @@ int epd_prepare(hipStream_t s)
   return BBM_HIP_OK;
 }
 
+// Device address of the table on the current device (the doubleRGB EPD kernels, f64.hip, get it as a parameter)
+const float* epd_table_device(hipStream_t s)
+{
+  if (epd_prepare(s)) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(g_epd_mutex);
+  return g_epd_tables[dev].dev;
+}
+
 // Host copy of the table (tests: compared with the reference's G1.h through the oracle shim).
 int epd_table_host(float* out, int capacity)
 {

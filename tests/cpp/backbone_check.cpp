@@ -210,7 +210,7 @@ int main()
   F64(bbm::nganblinnphong<D>) F64(bbm::lafortune<D>) F64(bbm::nganlafortune<D>) F64(bbm::ashikhminshirley<D>)
   F64(bbm::ashikhminshirleyfull<D>) F64(bbm::lowashikhminshirley<D>) F64(bbm::nganashikhminshirley<D>)
   F64(bbm::lowsmooth<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>) F64(bbm::bagher<D>)
-  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::bagher<D>>)
+  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::bagher<D>>) F64(epd_t<D>)
 #undef F64
 
   // an unknown model string fails loudly with the library's error

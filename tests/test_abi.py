@@ -54,9 +54,9 @@ def test_f64_registry(lib):
                  "LowMicrofacetFit", "Aggregate<Lambertian,CookTorrance>", "Aggregate<Lambertian,NganCookTorrance>"):
         assert has[name] == 1, name
     for name in ("Ward", "AshikhminShirleyFull", "LowSmooth", "Aggregate<Lambertian,NganWard>", "Bagher",
-                 "Aggregate<Lambertian,Bagher>"):
+                 "Aggregate<Lambertian,Bagher>", "EPD"):
         assert has[name] == 1, name
-    for name in ("HeWestin", "EPD", "Merl", "Aggregate<Lambertian,NganHe>"):
+    for name in ("HeWestin", "Merl", "Aggregate<Lambertian,NganHe>"):
         assert has[name] == 0, name
     assert lib.bbm_hip_model_has_f64(10_000) == -1
     # a model without doubleRGB kernels is refused before anything is launched

@@ -28,7 +28,9 @@ INP = ou.golden_inputs()
 TIGHT = 1e-10
 # Bagher's shadowing 1 + Lambda (1 - exp(c pow(theta - theta0, k))) cancels twice for published fits (c ~ 1e-7,
 # k ~ 48, G ~ 5e-4): an ulp of pow between ocml and glibc reaches the result amplified ~1e7 (measured 1.2e-9)
-TIGHT_MODEL = {"Bagher": 1e-7, "Aggregate<Lambertian,Bagher>": 1e-7}
+# EPD's shadowing table is regenerated on the device, not copied (epd.hpp): 4 % of its entries differ from the
+# reference's G1.h in the 6th printed digit, which the bilinear lookup passes on (~1e-6)
+TIGHT_MODEL = {"Bagher": 1e-7, "Aggregate<Lambertian,Bagher>": 1e-7, "EPD": 1e-5}
 
 
 @pytest.fixture(scope="module")
@@ -90,7 +92,7 @@ def test_f64_models_cover_the_analytic_families(bbm):
                  "WardDuer", "WardDuerGeislerMoroder", "NganWard", "NganWardDuer", "Phong", "NganBlinnPhong",
                  "Lafortune", "NganLafortune", "AshikhminShirley", "AshikhminShirleyFull", "LowAshikhminShirley",
                  "NganAshikhminShirley", "LowSmooth", "Aggregate<Lambertian,NganWardDuer>", "Bagher",
-                 "Aggregate<Lambertian,Bagher>"):
+                 "Aggregate<Lambertian,Bagher>", "EPD"):
         assert want in names, want
 
 
@@ -176,6 +178,14 @@ def _pdf_at_direction_proof(name, params, d_gpu, dout, p_gpu, k=4, trials=64, se
     return (lo <= p_gpu) & (p_gpu <= hi) | ou.parity_ok_f64(p_gpu, lo) | ou.parity_ok_f64(p_gpu, hi)
 
 
+def _dir_err(a, b):
+    """Per-lane max |a - b| over the three components; NaN where both are NaN counts as agreement, NaN on one
+    side as inf (EPD's sampler at xi1 = 0: the reference's own direction is NaN there)."""
+    d = np.abs(a - b)
+    d = np.where(np.isnan(a) & np.isnan(b), 0.0, np.where(np.isnan(d), np.inf, d))
+    return d.max(0)
+
+
 def _xi_ulps_proof(name, params, dout, xi, d_gpu, f_gpu, k=2):
     """Per-lane proof for a sample whose flag or direction differs from the reference's: the reference, given xi moved
     by <= k float steps per coordinate, returns the GPU's flag and a direction within 1e-5 -- the lane sits on a
@@ -193,7 +203,7 @@ def _xi_ulps_proof(name, params, dout, xi, d_gpu, f_gpu, k=2):
                     x[row] = np.nextafter(x[row], np.float32(np.inf if st > 0 else -np.inf))
             x = np.clip(x, 0, 1).astype(np.float32)
             d, _, f = ou.ref_sample_double(name, params, dout, x, nthreads=8)
-            ok |= (f == f_gpu.astype(np.uint32)) & (np.abs(d - d_gpu).max(0) <= 1e-5)
+            ok |= (f == f_gpu.astype(np.uint32)) & (_dir_err(d, d_gpu) <= 1e-5)
     return ok
 
 
@@ -216,7 +226,7 @@ def test_f64_sample(bbm, mode_out):
             d_gpu, p_gpu, f_gpu = s.direction.cpu().numpy(), s.pdf.cpu().numpy(), s.flag.cpu().numpy()
             d_ref, p_ref, f_ref = ou.ref_sample_double(name, g[f"params{si}"], dout, xi, nthreads=8)
             what = f"{name}[{si}] f64 sample {mode_out}"
-            derr = np.abs(d_gpu - d_ref).max(0)
+            derr = _dir_err(d_gpu, d_ref)
             off = np.nonzero((f_gpu.astype(np.uint32) != f_ref) | (derr > 1e-5))[0]
             by_xi = _xi_ulps_proof(name, g[f"params{si}"], dout[:, off], xi[:, off], d_gpu[:, off], f_gpu[off])
             assert by_xi.all(), (f"{what}: {int((~by_xi).sum())} samples off (flag / direction); lanes {off[~by_xi][:4]} "
@@ -224,7 +234,7 @@ def test_f64_sample(bbm, mode_out):
                                  f"{f_ref[off[~by_xi][:4]]}")
             # the proven lanes' pdfs are those of the GPU's own direction (checked by the pdf-at-direction proof)
             d_ref[:, off], p_ref[off] = d_gpu[:, off], np.nan
-            derr = np.abs(d_gpu - d_ref).max(0)
+            derr = _dir_err(d_gpu, d_ref)
             ok = ou.parity_ok_f64(p_gpu, p_ref)
             bad = np.nonzero(~ok)[0]
             proven = _pdf_at_direction_proof(name, g[f"params{si}"], d_gpu[:, bad], dout[:, bad], p_gpu[bad])
