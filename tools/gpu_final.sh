@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu > "$R/gpurun_out/final/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/final/prof.log"; exit 1; }
 cd "$R"
 bash tools/gpu_traffic.sh || exit 1
-for W in models sample fit; do
+for W in models sample fit f64; do
   timeout -k 10 300 python bench.py --workload $W --steps 10 --warmup 3 > gpurun_out/final/bench_$W.json 2> gpurun_out/final/bench_$W.err || { echo "bench $W failed"; tail -20 gpurun_out/final/bench_$W.err; exit 1; }
   cut -c1-200 gpurun_out/final/bench_$W.json
 done
