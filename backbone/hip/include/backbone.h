@@ -64,7 +64,7 @@ namespace bbm {
       static constexpr string_literal name = LABEL;
 
       //! \brief the device kernels evaluate this configuration: every model in f32 (floatRGB); in f64 (doubleRGB,
-      //! bbm_hip_*_f64) every analytic model but the He family, and their Aggregate(Lambertian, X) fits
+      //! bbm_hip_*_f64) every analytic model and their Aggregate(Lambertian, X) fits
       static constexpr bool device_batch = std::is_same_v<LANE, float> || std::is_same_v<LANE, double>;
 
       static Spectrum wavelength(void) { return {0.645, 0.526, 0.444}; }

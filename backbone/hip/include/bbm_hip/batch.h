@@ -568,7 +568,7 @@ namespace bbm {
 
     //! \brief doubleRGB (Value = double) models on f64 SoA arrays: eval + pdf, evaluated in f64 on the device
     //! (bbm_hip_eval_pdf_f64).  MODEL must have a single kernel (single model or fused aggregate) with doubleRGB
-    //! kernels (bbm_hip_model_has_f64: every analytic model but the He family, and their
+    //! kernels (bbm_hip_model_has_f64: every analytic model and their
     //! Aggregate(Lambertian, X) fits); any other model is rejected with BBM_HIP_ERR_UNSUPPORTED.
     template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
       inline void eval_pdf(const MODEL& model, soa3d in, soa3d out, size_t n, soa3d_out rgb, double* p,

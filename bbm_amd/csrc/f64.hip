@@ -116,24 +116,98 @@ template<class Model> struct grid_cap { static constexpr unsigned value = 0; };
 template<> struct grid_cap<RibardiereM> { static constexpr unsigned value = 2048; };
 template<> struct grid_cap<RibardiereAnisoM> { static constexpr unsigned value = 2048; };
 
-// Per-model host work before a launch: EPD's table address into its parameter slot (EpdNdf::kTableSlot)
-template<class Model> struct host_params { static int run(ParamBlockF64&, hipStream_t) { return 0; } };
+// Per-model host work before a launch, stream-ordered: EPD's table address into its parameter slot
+// (EpdNdf::kTableSlot); the He family's sampler CDF built into scratch, its address and component after the
+// model's parameters; an aggregate forwards to its second child with the slots shifted past the first's.
+template<class Model> struct host_params
+{
+  static int run(ParamBlockF64&, uint32_t, hipStream_t, void**) { return 0; }
+  static void done(void*, hipStream_t) {}
+};
 template<> struct host_params<EpdM>
 {
-  static int run(ParamBlockF64& p, hipStream_t s)
+  static int run(ParamBlockF64& p, uint32_t, hipStream_t s, void**)
   {
     const float* t = epd_table_device(s);
     if (!t) return fail(BBM_HIP_ERR_HIP, "EPD: shadowing table unavailable");
     p.v[EpdNdf::kTableSlot] = __builtin_bit_cast(double, reinterpret_cast<unsigned long long>(t));
     return 0;
   }
+  static void done(void*, hipStream_t) {}
+};
+
+// ndf::sampler::initialize (ndf/sampler.h:143-181) in double: 90 backscatter evaluations hsum(eval(h, h)) at
+// theta = (i / 90)^2 Pi/2, weighted by sin(theta1) sqrt(theta1), then cdf(samples) (util/cdf.h:39-47)
+template<class Model>
+__global__ __launch_bounds__(128) void k_he_cdf_f64(ParamBlockF64 p, uint32_t component, double* __restrict__ cdf)
+{
+  __shared__ double sm[90];
+  const Model m(p.v);
+  const int i = threadIdx.x;
+  if (i < 90)
+  {
+    const double q = double(i) / 90.0, q1 = double(i + 1) / 90.0;
+    const d3 h = sph_to_vec(0.0, (q * q) * (0.5 * kPi));
+    double rgb[3];
+    m.template eval_rgb<false>(h, h, component, rgb);
+    const double theta1 = (q1 * q1) * (0.5 * kPi);
+    sm[i] = (((0.0 + rgb[0]) + rgb[1]) + rgb[2]) / 1.0 * (sin(theta1) * sqrt(theta1));
+  }
+  __syncthreads();
+  if (i == 0)
+  {
+    double acc = 0.0;
+    for (int k = 0; k < 90; ++k) { acc += sm[k]; sm[k] = acc; }
+    for (int k = 0; k < 90; ++k) cdf[k] = sm[k] / acc;
+  }
+}
+
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
+{
+  using M = He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>;
+  static int run(ParamBlockF64& p, uint32_t component, hipStream_t s, void** scratch)
+  {
+    double* cdf = static_cast<double*>(scratch_acquire(90 * sizeof(double), s));
+    if (!cdf) return fail(BBM_HIP_ERR_HIP, "He (f64) sampler CDF: scratch allocation failed");
+    *scratch = cdf;
+    hipLaunchKernelGGL((k_he_cdf_f64<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
+    if (const int rc = launched("k_he_cdf_f64")) return rc;
+    p.v[M::kParams] = __builtin_bit_cast(double, reinterpret_cast<unsigned long long>(cdf));
+    p.v[M::kParams + 1] = double(component);
+    return 0;
+  }
+  static void done(void* scratch, hipStream_t s) { if (scratch) scratch_release(scratch, s); }
+};
+
+template<class A, class B>
+struct host_params<Aggregate<A, B>>
+{
+  static int run(ParamBlockF64& p, uint32_t component, hipStream_t s, void** scratch)
+  {
+    ParamBlockF64 q{};
+    for (int k = A::kParams; k < kMaxParamsF64; ++k) q.v[k - A::kParams] = p.v[k];
+    if (const int rc = host_params<B>::run(q, component, s, scratch)) return rc;
+    for (int k = A::kParams; k < kMaxParamsF64; ++k) p.v[k] = q.v[k - A::kParams];
+    return 0;
+  }
+  static void done(void* scratch, hipStream_t s) { host_params<B>::done(scratch, s); }
+};
+
+// releases a launch's scratch (stream-ordered) when the launcher returns
+template<class Model> struct Release
+{
+  void* p = nullptr;
+  hipStream_t s;
+  ~Release() { host_params<Model>::done(p, s); }
 };
 
 template<class Model>
 int launch_eval_pdf(const EvalArgsF64& a0, hipStream_t s)
 {
   EvalArgsF64 a = a0;
-  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
+  Release<Model> rel{nullptr, s};
+  if (const int rc = host_params<Model>::run(a.p, a.component, s, &rel.p)) return rc;
   const bool v2 = aligned16(a.ix) && aligned16(a.iy) && aligned16(a.iz) && aligned16(a.ox) && aligned16(a.oy) &&
                   aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
   unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
@@ -148,8 +222,7 @@ int launch_eval_pdf(const EvalArgsF64& a0, hipStream_t s)
 template<class Model>
 int launch_reflectance(const ReflArgsF64& a0, hipStream_t s)
 {
-  ReflArgsF64 a = a0;
-  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
+  ReflArgsF64 a = a0;     // reflectance reads no per-launch data (EPD: Fresnel only; He: Fresnel only)
   if (a.mask) hipLaunchKernelGGL((k_reflectance_f64<Model, true>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_reflectance_f64<Model, false>), dim3(grid(a.n)), dim3(kBlock), 0, s, a);
   return launched("k_reflectance_f64");
@@ -159,7 +232,8 @@ template<class Model>
 int launch_sample(const SampleArgsF64& a0, hipStream_t s)
 {
   SampleArgsF64 a = a0;
-  if (const int rc = host_params<Model>::run(a.p, s)) return rc;
+  Release<Model> rel{nullptr, s};
+  if (const int rc = host_params<Model>::run(a.p, a.component, s, &rel.p)) return rc;
   unsigned blocks = grid(a.n);
   if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
   if (a.mask) hipLaunchKernelGGL((k_sample_f64<Model, true>), dim3(blocks), dim3(kBlock), 0, s, a);
@@ -214,6 +288,11 @@ const Entry kF64[] = {
   BBM_HIP_F64("Bagher", Bagher),
   BBM_HIP_F64("Aggregate<Lambertian,Bagher>", AggBagherM),
   BBM_HIP_F64("EPD", EpdM),
+  BBM_HIP_F64("He", HeM),
+  BBM_HIP_F64("HeWestin", HeWestinM),
+  BBM_HIP_F64("HeHolzschuch", HeHolzschuchM),
+  BBM_HIP_F64("NganHe", NganHeM),
+  BBM_HIP_F64("Aggregate<Lambertian,NganHe>", AggNganHeM),
 };
 #undef BBM_HIP_F64
 
@@ -223,7 +302,7 @@ static_assert(Lambertian::kParams == 3 && OrenNayar::kParams == 4 && CookTorranc
               LowMicrofacetM::kParams == 6 && AggCookTorranceM::kParams == 8 && WardM::kParams == 5 &&
               NganWardM::kParams == 4 && PhongLobe::kParams == 4 && LafortuneM::kParams == 7 &&
               NganLafortuneM::kParams == 6 && ASM::kParams == 5 && ASFullM::kParams == 8 && LowASM::kParams == 5 &&
-              NganASM::kParams == 5 && LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4, "f64 nparams must match the floatRGB registry");
+              NganASM::kParams == 5 && LowSmooth::kParams == 6 && Bagher::kParams == 30 && EpdM::kParams == 4 && HeM::kParams == 8 && NganHeM::kParams == 6, "f64 nparams must match the floatRGB registry");
 
 }  // namespace
 

@@ -9,8 +9,8 @@
 //
 // Covered compositions: Lambertian, OrenNayar, every microfacet<NDF, G, F, N> composition of the floatRGB
 // registry (Beckmann / GGX / Phong / Student-T / Low NDFs x v-groove / uncorrelated / height-correlated x Cook /
-// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth), Bagher, EPD
-// and the Aggregate(Lambertian, X) fits of those.  Layout: SoA f64 (8 B per coordinate), two pairs per
+// Schlick Fresnel), the lobe models (Ward x 5, Phong, Lafortune x 2, Ashikhmin-Shirley x 4, LowSmooth), Bagher, EPD,
+// the He family and the Aggregate(Lambertian, X) fits of those: every analytic model.  Layout: SoA f64 (8 B per coordinate), two pairs per
 // thread with 16 B loads: 48 B in + 32 B out = 80 B per eval+pdf pair.
 #pragma once
 #include "math.hpp"
@@ -1160,6 +1160,220 @@ struct FresnelComplex
   }
 };
 
+// ------------------------------------------------------------------------------------------- the He family
+
+// doubleRGB::wavelength() (backbone/native/include/backbone.h:36), micron
+constexpr double kWavelength[3] = {0.645, 0.526, 0.444};
+
+__device__ __forceinline__ d3 sph_to_vec(double phi, double theta)    // spherical::convert (core/spherical.h)
+{
+  double st, ct, sp, cp;
+  sincos(theta, &st, &ct);
+  sincos(phi, &sp, &cp);
+  return mk(cp * st, sp * st, ct);
+}
+
+// ndf::sampler<NDF, 90, 1>::pdf (ndf/sampler.h:102-128) of the halfway vector m over a 90-entry double CDF
+__device__ __forceinline__ double ndf_sampler_pdf(const double* __restrict__ cdf, d3 m)
+{
+  const double theta = theta_of(m);
+  const double ti = sqrt(theta / (0.5 * kPi)) * 90 - 0.5;
+  const double w = ti - floor(ti);
+  const double fl = floor(ti), ce = ceil(ti);
+  // clamp(cast<Size_t>(floor(ti)), 0, 89): a negative value cast to size_t wraps (-> 89)
+  const int lidx = (fl < 0) ? 89 : int(fmin(fl, 89.0)), uidx = (ce < 0) ? 89 : int(fmin(ce, 89.0));
+  auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0); };
+  const double p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
+  const double jac = (sqrt(theta) * (0.25 * kPi * kPi) / 90) * fabs(sin(theta)) * (2.0 * kPi);
+  return ((m.z > 0) && (jac > kEps)) ? p / jac : 0.0;
+}
+
+// ndf::sampler::sample (ndf/sampler.h:63-92) with cdf::sample (util/cdf.h:73-83)
+__device__ __forceinline__ d3 ndf_sampler_halfway(const double* __restrict__ cdf, double xi0, double xi1)
+{
+  int idx = 0;
+  while (idx < 90 && cdf[idx] < xi0) ++idx;
+  const bool valid = idx < 90;
+  const double prev = (valid && idx >= 1) ? cdf[idx - 1] : 0.0;
+  const double residual = valid ? (xi0 - prev) / (cdf[idx] - prev) : 0.0;
+  const double off = 1 - safe_sqrt(1 - 2 * fabs(residual - 0.5));
+  const double q = (double(idx) + 0.5 + copysign(1.0, residual - 0.5) * off) / 90;
+  double theta = (q * q) * (0.5 * kPi);
+  theta = (theta > 0.5 * kPi) ? kPi - theta : theta;
+  return sph_to_vec(2.0 * kPi * xi1, theta);
+}
+
+// fresnel::complex<CONF, Spectrum> per channel (bbm/fresnel_complex.h:38-63); params n RGB, k RGB
+struct FresnelComplexRGB
+{
+  static constexpr int kParams = 6;
+  FresnelComplex f[3];
+  __device__ explicit FresnelComplexRGB(const double* q) : f{FresnelComplex(q), FresnelComplex(q), FresnelComplex(q)}
+  {
+    for (int c = 0; c < 3; ++c) { f[c].n = q[c]; f[c].k = q[3 + c]; }
+  }
+  __device__ __forceinline__ void eval3(double cs, double* F) const { for (int c = 0; c < 3; ++c) F[c] = f[c].eval(cs); }
+};
+struct FresnelCookRGB
+{
+  static constexpr int kParams = 1;
+  FresnelCook f;
+  __device__ explicit FresnelCookRGB(const double* q) : f(q) {}
+  __device__ __forceinline__ void eval3(double cs, double* F) const { F[0] = F[1] = F[2] = f.eval(cs); }
+};
+
+// he_base<...> (bsdfmodel/he.h:115-482) behind ndf_sampler (bbm/ndf_sampler.h:22-164), doubleRGB: every term in
+// double, Constants::Epsilon() the double epsilon (the adaptive Taylor stop included).  The sampler's 90-entry CDF
+// (double) is built per launch (k_he_cdf_f64) and its address and the component it was built for ride in the two
+// parameter slots after the model's own (as the floatRGB He, he.hpp).
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct He
+{
+  static constexpr int kOff = SCALED ? 3 : 0;
+  static constexpr int kParams = kOff + 2 + FRES::kParams;
+  static constexpr uint32_t kComponent = kFlagSpecular;
+  double albedo[3], sigma0, tau;
+  FRES fres;
+  const double* cdf;
+  uint32_t launch_component;
+  __device__ explicit He(const double* p) : sigma0(p[kOff]), tau(p[kOff + 1]), fres(p + kOff + 2)
+  {
+    for (int c = 0; c < 3; ++c) albedo[c] = SCALED ? p[c] : 1.0;
+    cdf = reinterpret_cast<const double*>(__builtin_bit_cast(unsigned long long, p[kParams]));
+    launch_component = uint32_t(p[kParams + 1]);
+  }
+  __device__ __forceinline__ bool masked(uint32_t component) const { return component != launch_component; }
+
+  // he.h:266-291, Eqs. 24-25
+  __device__ __forceinline__ double S1(d3 v) const
+  {
+    const double scot = tau * (1.0 / tan_theta(v)) / (2.0 * sigma0);
+    const double ec = 0.5 * erfc(scot);
+    double lambda = 0.5 * kInvSqrtPi / scot;
+    if (ERRATA) lambda *= exp(-(scot * scot));
+    lambda -= ec;
+    return (sigma0 < kEps) ? 1.0 : (1.0 - ec) / (lambda + 1.0);
+  }
+  // he.h:306-352, Eq. 76
+  __device__ __forceinline__ double G(d3 in, d3 out) const
+  {
+    const d3 v = mk(in.x + out.x, in.y + out.y, in.z + out.z);
+    const double vq = dot(v, v) / v.z;
+    const double v_scale = vq * vq;
+    const double kixn2 = 1 - in.z * in.z, krxn2 = 1 - out.z * out.z;
+    const double kikr = dot(mk(-in.x, -in.y, -in.z), out);
+    const double sikr = out.y * in.x - out.x * in.y, srki = in.y * out.x - in.x * out.y;
+    const double pikr = out.z + kikr * in.z, prki = in.z + kikr * out.z;
+    const double dd = 1.0 - kikr * kikr;
+    const double denom = dd * dd;
+    const double nom = (sikr * sikr + pikr * pikr) * (srki * srki + prki * prki) / (krxn2 * kixn2);
+    return (denom > kEps) ? v_scale * nom / denom : 1.0;
+  }
+  // he.h:365-400, Eq. 80 by 4 Newton-Raphson steps
+  __device__ __forceinline__ double sigma(d3 in, d3 out) const
+  {
+    const double ti = tan_theta(in), to = tan_theta(out);
+    auto K = [&](double t) { return t * erfc(tau / (2 * sigma0 * t)); };
+    const double Ki = (ti > kEps) ? K(ti) : 0.0, Ko = (to > kEps) ? K(to) : 0.0;
+    const double f0 = (1.0 / sqrt(8.0 * kPi)) * (Ki + Ko);
+    double x = (f0 <= 1.0) ? f0 : safe_sqrt(2.0 * log(f0));
+    for (int s = 0; s < 4; ++s)
+    {
+      const double expn = exp(0.5 * x * x);
+      const double ev = x * expn - f0, grad = (1 + x * x) * expn;
+      x -= (grad > kEps) ? ev / grad : 0.0;
+    }
+    return (sigma0 > kEps) ? sigma0 / safe_sqrt(1 + x * x) : 0.0;
+  }
+  // he.h:411-467, Eqs. 78-79
+  __device__ __forceinline__ void D(d3 in, d3 out, double* Dout) const
+  {
+    const double vxy2 = sqnorm2(in.x + out.x, in.y + out.y);
+    const double sg = sigma(in, out);
+    const double tau2 = tau * tau;
+    double g[3], eb[3], norm[3];
+    for (int c = 0; c < 3; ++c)
+    {
+      const double gg = 2.0 * kPi * sg * (in.z + out.z) / kWavelength[c];
+      g[c] = gg * gg;
+      const double l2 = kWavelength[c] * kWavelength[c];
+      norm[c] = 0.25 * kPi * kPi * tau2 / l2;
+      eb[c] = vxy2 * tau2 / 4;
+      if (WESTIN) eb[c] *= 4.0 * kPi * kPi / l2;
+    }
+    const double gmin = fmin(fmin(g[0], g[1]), g[2]);
+    double rough[3] = {0.0, 0.0, 0.0}, weight = 0.0;
+    if (APPROX >= 0 && gmin > double(APPROX))
+    {
+      for (int c = 0; c < 3; ++c) rough[c] = exp(-eb[c] / g[c]) / g[c];
+      weight = fmin(fmax(gmin - double(APPROX), 0.0), 1.0);
+    }
+    double sum[3] = {0.0, 0.0, 0.0}, gm[3] = {1.0, 1.0, 1.0}, term[3] = {0.0, 0.0, 0.0}, last[3];
+    bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
+    for (int m = 1; m <= TAYLOR && !converged; ++m)
+    {
+      for (int c = 0; c < 3; ++c)
+      {
+        last[c] = term[c];
+        gm[c] *= g[c] / m;
+        term[c] = exp(-g[c] - eb[c] / m) * gm[c] / m;
+        sum[c] += term[c];
+      }
+      if (ADAPTIVE)
+      {
+        const double t = fmin(fmin(term[0], term[1]), term[2]);
+        converged = (t < kEps) && (t < fmin(fmin(last[0], last[1]), last[2]));
+      }
+    }
+    for (int c = 0; c < 3; ++c) Dout[c] = norm[c] * lerp(sum[c], rough[c], weight);
+  }
+  // he_base::eval (he.h:142-166) [x albedo, scaledmodel.h:50-53; the sampler sees the unscaled he_base]
+  template<bool SCALE = true>
+  __device__ __forceinline__ void eval_rgb(d3 in, d3 out, uint32_t component, double* rgb) const
+  {
+    const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    double Dv[3], F[3];
+    const double S = S1(in) * S1(out);
+    const double Gv = G(in, out);
+    D(in, out, Dv);
+    fres.eval3(safe_sqrt((1 + dot(in, out)) / 2.0), F);
+    const double nrm = 1.0 / (kPi * in.z * out.z);
+    for (int c = 0; c < 3; ++c)
+    {
+      double v = nrm * F[c] * S * Gv * Dv[c];
+      if (SCALED && SCALE) v *= albedo[c];
+      rgb[c] = active ? v : 0.0;
+    }
+  }
+  // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156): sampler pdf of h / |4 out.h|
+  __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
+  {
+    eval_rgb(in, out, component, rgb);
+    const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
+    const bool active = (out.z > 0) && (in.z > 0) && !masked(component);
+    pdf = active ? ndf_sampler_pdf(cdf, h) / fabs(4.0 * dot(out, h)) : 0.0;
+  }
+  // he.h:230-244
+  __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
+  {
+    const bool m = (component & kFlagSpecular) && (out.z > 0);
+    double F[3];
+    fres.eval3(out.z, F);
+    for (int c = 0; c < 3; ++c) rgb[c] = m ? (SCALED ? F[c] / kPi * 4.0 * albedo[c] : F[c] / kPi * 4.0) : 0.0;
+  }
+  // ndf_sampler::sample (bbm/ndf_sampler.h:78-111)
+  __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
+                                         uint32_t& flag) const
+  {
+    dir = mk(0.0, 0.0, 0.0); pdf = 0.0; flag = kFlagNone;
+    if (!(xi_ok(xi0, xi1) && (out.z > 0)) || masked(component)) return;
+    dir = reflect(out, ndf_sampler_halfway(cdf, xi0, xi1));
+    double rgb[3];
+    eval_pdf(dir, out, component, rgb, pdf);
+    flag = component;
+  }
+};
+
 // Compositions (the floatRGB registry's, models.hpp)
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;
@@ -1195,6 +1409,11 @@ using AggNganWardM = Aggregate<Lambertian, NganWardM>;
 using AggNganWardDuerM = Aggregate<Lambertian, NganWardDuerM>;
 using AggBagherM = Aggregate<Lambertian, Bagher>;
 using EpdM = Microfacet<EpdNdf, VanGinneken, FresnelComplex, Norm::Walter, false>;   // holzschuchpacanowski.h:34-42
+using HeM = He<FresnelComplexRGB, false, false, 64, true, 18, false>;      // he.h:489-496
+using HeWestinM = He<FresnelComplexRGB, true, true, 64, true, 18, false>;
+using HeHolzschuchM = He<FresnelComplexRGB, true, false, 10, false, -1, false>;
+using NganHeM = He<FresnelCookRGB, true, true, 64, true, 18, true>;        // ngan.h:166-167
+using AggNganHeM = Aggregate<Lambertian, NganHeM>;
 
 // ------------------------------------------------------------------------------------------------- kernels
 

@@ -122,7 +122,7 @@ int bbm_hip_reflectance(int model_id, const float* params, int nparams,
 
 /* The reference's doubleRGB configuration (backbone/native/include/backbone.h:41-42: Value = double, Spectrum =
  * color<double>): the same calls on SoA float64 arrays with a double parameter vector, evaluated in f64 on the
- * device.  Available for the models bbm_hip_model_has_f64 reports (every analytic model but the He family, and their Aggregate(Lambertian, X) fits); BBM_HIP_ERR_UNSUPPORTED for the others. */
+ * device.  Available for the models bbm_hip_model_has_f64 reports (every analytic model and their Aggregate(Lambertian, X) fits); BBM_HIP_ERR_UNSUPPORTED for the others. */
 int bbm_hip_model_has_f64(int model_id);                /* 1 / 0, <0 for an unknown id */
 int bbm_hip_eval_pdf_f64(int model_id, const double* params, int nparams,
                          const double* in_x, const double* in_y, const double* in_z,

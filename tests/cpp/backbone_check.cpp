@@ -211,6 +211,8 @@ int main()
   F64(bbm::ashikhminshirleyfull<D>) F64(bbm::lowashikhminshirley<D>) F64(bbm::nganashikhminshirley<D>)
   F64(bbm::lowsmooth<D>) F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::nganwardduer<D>>) F64(bbm::bagher<D>)
   F64(bbm::aggregatemodel<bbm::lambertian<D>, bbm::bagher<D>>) F64(epd_t<D>)
+  F64(bbmref::he<D>) F64(bbmref::hewestin<D>) F64(bbmref::heholzschuch<D>) F64(bbmref::nganhe<D>)
+  F64(bbm::aggregatemodel<bbm::lambertian<D>, bbmref::nganhe<D>>)
 #undef F64
 
   // an unknown model string fails loudly with the library's error

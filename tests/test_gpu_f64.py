@@ -30,7 +30,9 @@ TIGHT = 1e-10
 # k ~ 48, G ~ 5e-4): an ulp of pow between ocml and glibc reaches the result amplified ~1e7 (measured 1.2e-9)
 # EPD's shadowing table is regenerated on the device, not copied (epd.hpp): 4 % of its entries differ from the
 # reference's G1.h in the 6th printed digit, which the bilinear lookup passes on (~1e-6)
-TIGHT_MODEL = {"Bagher": 1e-7, "Aggregate<Lambertian,Bagher>": 1e-7, "EPD": 1e-5}
+# The He family's Taylor series sums up to 64 terms of e^(-g - eb/m) g^m / m!, m m: measured 2.9e-11.
+TIGHT_MODEL = {"Bagher": 1e-7, "Aggregate<Lambertian,Bagher>": 1e-7, "EPD": 1e-5, "He": 1e-9, "HeWestin": 1e-9,
+               "HeHolzschuch": 1e-9, "NganHe": 1e-9, "Aggregate<Lambertian,NganHe>": 1e-9}
 
 
 @pytest.fixture(scope="module")
@@ -92,7 +94,8 @@ def test_f64_models_cover_the_analytic_families(bbm):
                  "WardDuer", "WardDuerGeislerMoroder", "NganWard", "NganWardDuer", "Phong", "NganBlinnPhong",
                  "Lafortune", "NganLafortune", "AshikhminShirley", "AshikhminShirleyFull", "LowAshikhminShirley",
                  "NganAshikhminShirley", "LowSmooth", "Aggregate<Lambertian,NganWardDuer>", "Bagher",
-                 "Aggregate<Lambertian,Bagher>", "EPD"):
+                 "Aggregate<Lambertian,Bagher>", "EPD", "He", "HeWestin", "HeHolzschuch", "NganHe",
+                 "Aggregate<Lambertian,NganHe>"):
         assert want in names, want
 
 
@@ -275,8 +278,10 @@ def test_f64_mask_unaligned_and_odd_sizes(bbm):
 def test_f64_unsupported_and_bad_arguments(bbm):
     from bbm_amd import _lib
     din = bbm.fill_directions(1, 0, 0, 64, mode=0).double()
+    # Merl (measured data) has no doubleRGB kernels: refused before anything is launched
     with pytest.raises(_lib.BackboneError) as e:
-        bbm.BsdfModel("HeWestin").eval_pdf(din, din)
+        _lib.check(_lib.load().bbm_hip_eval_pdf_f64(_lib.load().bbm_hip_model_id(b"Merl"), None, 2, None, None, None,
+                                                    None, None, None, None, 0, 3, 0, None, None, None, None, None))
     assert e.value.code == _lib.ERR_UNSUPPORTED
     m = bbm.CookTorrance()
     with pytest.raises(TypeError):
