@@ -17,8 +17,9 @@
  * enoki/drjit backbones' floatPacketRGB), because the device batch IS the packet, laid out SoA in HBM.
  *
  * Configurations (backbone.cmake BBM_BACKBONE_CONFIGURATIONS): floatRGB (device kernels compute in f32 with the
- * native backbone's rounding) and doubleRGB (host only: the device adapter static_asserts Value ==
- * float).
+ * native backbone's rounding) and doubleRGB (device kernels in f64 for every analytic model, their
+ * Aggregate(Lambertian, X) fits and any composed aggregate of those: the soa3d overloads of bbm_hip/batch.h,
+ * DESIGN.md §4.12).
  */
 #ifndef _BBM_HIP_BACKBONE_H_
 #define _BBM_HIP_BACKBONE_H_

@@ -15,8 +15,8 @@
  *      (include/bbm/bsdf_enumerate.h), i.e. in declaration order, and passed by value.
  * The runtime handle bsdf_ptr<C> (include/bbm/bsdf_ptr.h:21-165, what checkBsdf and the Mitsuba plugin hold)
  * is mapped through its toString() and the library's parser of the reference's model strings
- * (bbm_hip_parse_model): a single model or fused aggregate runs its kernel, any other aggregate (including the
- * runtime aggregatebsdf) runs composed from its children's kernels (bbm_hip_aggregate_*).
+ * (bbm_hip_parse_model_tree): a single model or fused aggregate runs its kernel, any other aggregate (including
+ * the runtime aggregatebsdf, nested to any depth) runs composed from its children's kernels (bbm_hip_aggregate_*).
  * Device buffers are caller-owned SoA float arrays; calls are asynchronous on `stream`.  Errors from the C-ABI
  * are rethrown as bbm::hip::error (a std::runtime_error), matching the reference's exception style
  * (include/core/error.h:42-46).
@@ -271,6 +271,14 @@ namespace bbm {
       template<typename M> struct aggregate_of { static constexpr bool value = false; };
 #endif
 
+      //! \brief an aggregate with an aggregate child: no fused kernel, and the reference cannot reflect its
+      //! attributes as a whole (util/reflection.h:247), so it is described child by child
+      template<typename M> struct nested_aggregate : std::false_type {};
+#ifdef _BBM_AGGREGATEMODEL_H_
+      template<auto NM, typename... X>
+        struct nested_aggregate<bbm::aggregatemodel_base<NM, X...>> : std::bool_constant<(aggregate_of<X>::value || ...)> {};
+#endif
+
       //! \brief calls f.template operator()<X>() for every type of a std::tuple<X...> (no instance is built)
       template<typename F, typename... X>
         inline void for_each_type(F&& f, const std::tuple<X...>*) { (f.template operator()<X>(), ...); }
@@ -354,20 +362,55 @@ namespace bbm {
     } // end detail namespace
 #endif
 
-    //! \brief A model as the library sees it: one registry entry (single model / fused aggregate) or the
-    //! children of a composed aggregate, each with its parameter vector.
-    struct model_desc
+    //! \brief A model as the library sees it: one registry entry (single model / fused aggregate) with its
+    //! parameter vector, or a composed aggregate (id = BBM_HIP_AGGREGATE) whose children are model_descs again --
+    //! aggregatemodel_base takes any bsdfmodel child (aggregatemodel.h:22), another aggregate included.  T: the
+    //! configuration's Value (float: floatRGB, double: doubleRGB).
+    template<typename T>
+      struct basic_model_desc
     {
-      std::vector<int> ids;
-      std::vector<std::vector<float>> params;
-      bool composed(void) const { return ids.size() > 1; }
-      std::vector<bbm_hip_child> children(void) const
-      {
-        std::vector<bbm_hip_child> c(ids.size());
-        for(size_t k = 0; k < ids.size(); ++k) c[k] = {ids[k], params[k].data(), int(params[k].size())};
-        return c;
-      }
+      int id = -1;
+      std::vector<T> params;
+      std::vector<basic_model_desc> kids;
+      bool composed(void) const { return id == BBM_HIP_AGGREGATE; }
     };
+    using model_desc = basic_model_desc<float>;
+    using model_desc_f64 = basic_model_desc<double>;
+
+    namespace detail {
+      template<typename T> struct child_of { using type = bbm_hip_child; };
+      template<> struct child_of<double> { using type = bbm_hip_child_f64; };
+
+      //! \brief the C-ABI child arrays of a composed model_desc (nested arrays for nested aggregates), kept alive
+      //! as long as this object
+      template<typename T>
+        struct child_tree
+      {
+        using child_t = typename child_of<T>::type;
+        std::vector<std::vector<child_t>> store;
+        const child_t* root = nullptr;
+        int count = 0;
+        explicit child_tree(const basic_model_desc<T>& m)
+        {
+          store.reserve(64);
+          root = build(m);
+          count = int(m.kids.size());
+        }
+        const child_t* build(const basic_model_desc<T>& m)
+        {
+          std::vector<child_t> v(m.kids.size());
+          for(size_t k = 0; k < m.kids.size(); ++k)
+          {
+            const auto& c = m.kids[k];
+            if(c.composed()) v[k] = child_t{BBM_HIP_AGGREGATE, nullptr, 0, build(c), int(c.kids.size())};
+            else v[k] = child_t{c.id, c.params.data(), int(c.params.size()), nullptr, 0};
+          }
+          if(store.size() == store.capacity()) throw error(BBM_HIP_ERR_INVALID_ARG, "aggregate tree too large");
+          store.push_back(std::move(v));      // capacity reserved: earlier arrays never move
+          return store.back().data();
+        }
+      };
+    } // end detail namespace
 
     //! \brief model_desc of a model string (bsdf_ptr toString, a fits/ entry) via the library's parser
     inline model_desc from_string(const std::string& s)
@@ -381,31 +424,36 @@ namespace bbm {
         std::vector<float> p(2);
         std::memcpy(&p[0], &lo, 4);
         std::memcpy(&p[1], &hi, 4);
-        return model_desc{{id_of("Merl")}, {p}};
+        return model_desc{id_of("Merl"), p, {}};
       }
 #endif
-      std::vector<int> ids(64), np(64);
-      std::vector<float> buf(64 * 64);
-      const int k = bbm_hip_parse_model(s.c_str(), ids.data(), buf.data(), np.data(), 64, int(buf.size()));
+      std::vector<int> ids(256), nk(256), np(256);
+      std::vector<float> buf(256 * 64);
+      const int k = bbm_hip_parse_model_tree(s.c_str(), ids.data(), nk.data(), buf.data(), np.data(), 256, int(buf.size()));
       check(k);
-      model_desc d;
-      size_t off = 0;
-      for(int c = 0; c < k; ++c)
-      {
-        d.ids.push_back(ids[size_t(c)]);
-        d.params.emplace_back(buf.begin() + long(off), buf.begin() + long(off + size_t(np[size_t(c)])));
-        off += size_t(np[size_t(c)]);
-      }
+      // preorder -> tree
+      size_t node = 0, off = 0;
+      auto take = [&](auto&& self) -> model_desc {
+        model_desc d;
+        d.id = ids[node];
+        d.params.assign(buf.begin() + long(off), buf.begin() + long(off + size_t(np[node])));
+        off += size_t(np[node]);
+        const int nkids = nk[node++];
+        for(int c = 0; c < nkids; ++c) d.kids.push_back(self(self));
+        return d;
+      };
+      model_desc d = take(take);
+      if(int(node) != k) throw error(BBM_HIP_ERR_INVALID_ARG, "malformed model tree from the parser");
       return d;
     }
 
-    //! \brief model_desc of a model instance, resolved by type (compile-time dispatch)
-    template<typename MODEL>
-      inline model_desc describe(const MODEL& model)
+    //! \brief model_desc of a model instance, resolved by type (compile-time dispatch); T = float for floatRGB
+    //! models (float32 entry points), double for doubleRGB models (the *_f64 entry points)
+    template<typename T, typename MODEL>
+      inline basic_model_desc<T> describe_as(const MODEL& model)
     {
       using M = std::decay_t<MODEL>;
-      static_assert(std::is_same_v<Value_t<get_config<M>>, float>,
-                    "float32 entry points take floatRGB-style models; doubleRGB models use the soa3d overloads");
+      static_assert(std::is_same_v<Value_t<get_config<M>>, T>, "the model's Value type must match the entry points");
 #ifdef _BBM_MERL_H_
       // Merl: ndf_sampler<merl_data<C, "Merl">, 90, 1> (staticmodel/merl.h:224-225), identified by its file
       // (toString, merl.h:161-164); a bare merl_data (placeholder sampler, merl.h:108-115) is rejected
@@ -414,26 +462,44 @@ namespace bbm {
       {
         static_assert(!std::is_same_v<M, decltype(detail::merl_base_of(static_cast<const M*>(nullptr)))>,
                       "merl_data without its data-driven sampler has no HIP kernel; use bbm::merl<CONF>");
+        static_assert(std::is_same_v<T, float>, "Merl is a floatRGB model on the device (DESIGN.md §7)");
         return from_string(bbm::toString(model));
       }
       else
 #endif
       if constexpr (detail::aggregate_of<M>::value)
       {
-        const std::string key = detail::single_name<M>();
-        const int fused = bbm_hip_model_id(key.c_str());
-        if(fused >= 0) return model_desc{{fused}, {parameters(model)}};
-        // composed: each child (a base class of the aggregate) with its own kernel and parameters
-        model_desc d;
-        detail::for_each_type([&]<typename X>() {
-          const model_desc c = describe(static_cast<const X&>(model));
-          if(c.composed()) throw error(BBM_HIP_ERR_UNSUPPORTED, "nested aggregates are not supported");
-          d.ids.push_back(c.ids[0]);
-          d.params.push_back(c.params[0]);
-        }, static_cast<const typename detail::aggregate_of<M>::children*>(nullptr));
+        if constexpr (!detail::nested_aggregate<M>::value)
+        {
+          const std::string key = detail::single_name<M>();
+          const int fused = bbm_hip_model_id(key.c_str());
+          if(fused >= 0)
+          {
+            if constexpr (std::is_same_v<T, float>) return basic_model_desc<T>{fused, parameters(model), {}};
+            else return basic_model_desc<T>{fused, parameters_f64(model), {}};
+          }
+        }
+        // composed: each child (a base class of the aggregate) with its own kernel(s) -- a nested aggregate stays
+        // one child, composed in turn
+        basic_model_desc<T> d;
+        d.id = BBM_HIP_AGGREGATE;
+        detail::for_each_type([&]<typename X>() { d.kids.push_back(describe_as<T>(static_cast<const X&>(model))); },
+                              static_cast<const typename detail::aggregate_of<M>::children*>(nullptr));
         return d;
       }
-      else return model_desc{{id_of(detail::single_name<M>())}, {parameters(model)}};
+      else
+      {
+        if constexpr (std::is_same_v<T, float>) return basic_model_desc<T>{id_of(detail::single_name<M>()), parameters(model), {}};
+        else return basic_model_desc<T>{id_of(detail::single_name<M>()), parameters_f64(model), {}};
+      }
+    }
+
+    template<typename MODEL>
+      inline model_desc describe(const MODEL& model)
+    {
+      static_assert(std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, float>,
+                    "float32 entry points take floatRGB-style models; doubleRGB models use the soa3d overloads");
+      return describe_as<float>(model);
     }
 
 #ifdef _BBM_BSDF_PTR_H_
@@ -458,12 +524,12 @@ namespace bbm {
     {
       if(m.composed())
       {
-        const auto c = m.children();
-        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+        const detail::child_tree<float> c(m);
+        check(bbm_hip_aggregate_eval_pdf(c.root, c.count, in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
                                          uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, pdf, stream));
       }
       else
-        check(bbm_hip_eval_pdf(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+        check(bbm_hip_eval_pdf(m.id, m.params.data(), int(m.params.size()), in.x, in.y, in.z, out.x, out.y,
                                out.z, mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, pdf, stream));
     }
 
@@ -474,12 +540,12 @@ namespace bbm {
     {
       if(m.composed())
       {
-        const auto c = m.children();
-        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+        const detail::child_tree<float> c(m);
+        check(bbm_hip_aggregate_eval_pdf(c.root, c.count, in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
                                          uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, nullptr, stream));
       }
       else
-        check(bbm_hip_eval(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+        check(bbm_hip_eval(m.id, m.params.data(), int(m.params.size()), in.x, in.y, in.z, out.x, out.y,
                            out.z, mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
     }
 
@@ -490,12 +556,12 @@ namespace bbm {
     {
       if(m.composed())
       {
-        const auto c = m.children();
-        check(bbm_hip_aggregate_eval_pdf(c.data(), int(c.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+        const detail::child_tree<float> c(m);
+        check(bbm_hip_aggregate_eval_pdf(c.root, c.count, in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
                                          uint32_t(component), uint32_t(unit), nullptr, nullptr, nullptr, pdf, stream));
       }
       else
-        check(bbm_hip_pdf(m.ids[0], m.params[0].data(), int(m.params[0].size()), in.x, in.y, in.z, out.x, out.y,
+        check(bbm_hip_pdf(m.id, m.params.data(), int(m.params.size()), in.x, in.y, in.z, out.x, out.y,
                           out.z, mask, n, uint32_t(component), uint32_t(unit), pdf, stream));
     }
 
@@ -507,13 +573,13 @@ namespace bbm {
     {
       if(m.composed())
       {
-        const auto c = m.children();
-        check(bbm_hip_aggregate_sample(c.data(), int(c.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
+        const detail::child_tree<float> c(m);
+        check(bbm_hip_aggregate_sample(c.root, c.count, out.x, out.y, out.z, xi0, xi1, mask, n,
                                        uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf,
                                        flag, stream));
       }
       else
-        check(bbm_hip_sample(m.ids[0], m.params[0].data(), int(m.params[0].size()), out.x, out.y, out.z, xi0, xi1, mask,
+        check(bbm_hip_sample(m.id, m.params.data(), int(m.params.size()), out.x, out.y, out.z, xi0, xi1, mask,
                              n, uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, pdf, flag,
                              stream));
     }
@@ -525,12 +591,12 @@ namespace bbm {
     {
       if(m.composed())
       {
-        const auto c = m.children();
-        check(bbm_hip_aggregate_reflectance(c.data(), int(c.size()), out.x, out.y, out.z, mask, n, uint32_t(component),
+        const detail::child_tree<float> c(m);
+        check(bbm_hip_aggregate_reflectance(c.root, c.count, out.x, out.y, out.z, mask, n, uint32_t(component),
                                             uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
       }
       else
-        check(bbm_hip_reflectance(m.ids[0], m.params[0].data(), int(m.params[0].size()), out.x, out.y, out.z, mask, n,
+        check(bbm_hip_reflectance(m.id, m.params.data(), int(m.params.size()), out.x, out.y, out.z, mask, n,
                                   uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
     }
 
@@ -566,45 +632,77 @@ namespace bbm {
                               const uint8_t* mask=nullptr, void* stream=nullptr)
     { reflectance(describe(model), out, n, rgb, component, unit, mask, stream); }
 
-    //! \brief doubleRGB (Value = double) models on f64 SoA arrays: eval + pdf, evaluated in f64 on the device
-    //! (bbm_hip_eval_pdf_f64).  MODEL must have a single kernel (single model or fused aggregate) with doubleRGB
-    //! kernels (bbm_hip_model_has_f64: every analytic model and their
-    //! Aggregate(Lambertian, X) fits); any other model is rejected with BBM_HIP_ERR_UNSUPPORTED.
+    //! \brief doubleRGB (Value = double) model_desc on f64 SoA arrays: eval + pdf evaluated in f64 on the device
+    //! (bbm_hip_eval_pdf_f64, or bbm_hip_aggregate_eval_pdf_f64 for a composed aggregate).  Every leaf must have
+    //! doubleRGB kernels (bbm_hip_model_has_f64: every analytic model and their Aggregate(Lambertian, X) fits);
+    //! any other is rejected with BBM_HIP_ERR_UNSUPPORTED.
+    inline void eval_pdf(const model_desc_f64& m, soa3d in, soa3d out, size_t n, soa3d_out rgb, double* p,
+                         bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                         const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const detail::child_tree<double> c(m);
+        check(bbm_hip_aggregate_eval_pdf_f64(c.root, c.count, in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
+                                             uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, p, stream));
+      }
+      else
+        check(bbm_hip_eval_pdf_f64(m.id, m.params.data(), int(m.params.size()), in.x, in.y, in.z, out.x, out.y, out.z,
+                                   mask, n, uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, p, stream));
+    }
+
+    //! \brief doubleRGB sample of N (out, xi) -> direction, pdf, flag (bbm_hip_sample_f64 / _aggregate_sample_f64)
+    inline void sample(const model_desc_f64& m, soa3d out, const double* xi0, const double* xi1, size_t n,
+                       soa3d_out direction, double* p, uint32_t* flag,
+                       bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                       const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const detail::child_tree<double> c(m);
+        check(bbm_hip_aggregate_sample_f64(c.root, c.count, out.x, out.y, out.z, xi0, xi1, mask, n, uint32_t(component),
+                                           uint32_t(unit), direction.x, direction.y, direction.z, p, flag, stream));
+      }
+      else
+        check(bbm_hip_sample_f64(m.id, m.params.data(), int(m.params.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
+                                 uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, p, flag, stream));
+    }
+
+    //! \brief doubleRGB reflectance of N out directions (bbm_hip_reflectance_f64 / _aggregate_reflectance_f64)
+    inline void reflectance(const model_desc_f64& m, soa3d out, size_t n, soa3d_out rgb,
+                            bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
+                            const uint8_t* mask=nullptr, void* stream=nullptr)
+    {
+      if(m.composed())
+      {
+        const detail::child_tree<double> c(m);
+        check(bbm_hip_aggregate_reflectance_f64(c.root, c.count, out.x, out.y, out.z, mask, n, uint32_t(component),
+                                                uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+      }
+      else
+        check(bbm_hip_reflectance_f64(m.id, m.params.data(), int(m.params.size()), out.x, out.y, out.z, mask, n,
+                                      uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
+    }
+
+    // ... and on doubleRGB model instances (template API), single, fused or composed
     template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
       inline void eval_pdf(const MODEL& model, soa3d in, soa3d out, size_t n, soa3d_out rgb, double* p,
                            bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                            const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      static const int id = id_of(detail::single_name<MODEL>());
-      const std::vector<double> prm = parameters_f64(model);
-      check(bbm_hip_eval_pdf_f64(id, prm.data(), int(prm.size()), in.x, in.y, in.z, out.x, out.y, out.z, mask, n,
-                                 uint32_t(component), uint32_t(unit), rgb.x, rgb.y, rgb.z, p, stream));
-    }
+    { eval_pdf(describe_as<double>(model), in, out, n, rgb, p, component, unit, mask, stream); }
 
-    //! \brief doubleRGB sample of N (out, xi) -> direction, pdf, flag (bbm_hip_sample_f64)
     template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
       inline void sample(const MODEL& model, soa3d out, const double* xi0, const double* xi1, size_t n,
                          soa3d_out direction, double* p, uint32_t* flag,
                          bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                          const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      static const int id = id_of(detail::single_name<MODEL>());
-      const std::vector<double> prm = parameters_f64(model);
-      check(bbm_hip_sample_f64(id, prm.data(), int(prm.size()), out.x, out.y, out.z, xi0, xi1, mask, n,
-                               uint32_t(component), uint32_t(unit), direction.x, direction.y, direction.z, p, flag, stream));
-    }
+    { sample(describe_as<double>(model), out, xi0, xi1, n, direction, p, flag, component, unit, mask, stream); }
 
-    //! \brief doubleRGB reflectance of N out directions (bbm_hip_reflectance_f64)
     template<typename MODEL> requires std::is_same_v<Value_t<get_config<std::decay_t<MODEL>>>, double>
       inline void reflectance(const MODEL& model, soa3d out, size_t n, soa3d_out rgb,
                               bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance,
                               const uint8_t* mask=nullptr, void* stream=nullptr)
-    {
-      static const int id = id_of(detail::single_name<MODEL>());
-      const std::vector<double> prm = parameters_f64(model);
-      check(bbm_hip_reflectance_f64(id, prm.data(), int(prm.size()), out.x, out.y, out.z, mask, n, uint32_t(component),
-                                    uint32_t(unit), rgb.x, rgb.y, rgb.z, stream));
-    }
+    { reflectance(describe_as<double>(model), out, n, rgb, component, unit, mask, stream); }
 
     //! \brief Sample losses of include/loss/*.h, for loss_sums
     enum class loss_t : int { nganL2 = BBM_LOSS_NGAN_L2, lowL2 = BBM_LOSS_LOW_L2, bieronL2 = BBM_LOSS_BIERON_L2,
@@ -616,14 +714,15 @@ namespace bbm {
     //! sums[p] = sum_i loss(model(probes[p]).eval(in_i, out_i), ref_i) in double (device).  Divide by the
     //! linearizer size (after summing the shards of all GPUs) for the reference's loss value.  MODEL must have a
     //! single kernel (single model or fused aggregate).
+    //! COMPONENT and UNIT are sampledlossfunction's template arguments (sampledlossfunction.h:34, :70-71).
     template<typename MODEL>
       inline void loss_sums(const MODEL& model, const float* probes, int nprobes, soa3 in, soa3 out, size_t n,
                             soa3 ref, loss_t loss, double* sums, void* workspace, size_t workspace_bytes,
-                            bsdf_flag component=bsdf_flag::All, void* stream=nullptr)
+                            bsdf_flag component=bsdf_flag::All, unit_t unit=unit_t::Radiance, void* stream=nullptr)
     {
       const int np = int(parameters(model).size());
       check(bbm_hip_loss_pairs(model_id<MODEL>(), probes, np, nprobes, n, in.x, in.y, in.z, out.x, out.y, out.z,
-                               ref.x, ref.y, ref.z, int(loss), uint32_t(component), 0u, sums, workspace,
+                               ref.x, ref.y, ref.z, int(loss), uint32_t(component), uint32_t(unit), sums, workspace,
                                workspace_bytes, stream));
     }
 

@@ -63,12 +63,29 @@ SIGNATURES = {
     "bbm_hip_aggregate_reflectance": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
     "bbm_hip_model_layout": (ctypes.c_char_p, [_I]),
     "bbm_hip_parse_model": (_I, [ctypes.c_char_p, _P, _P, _P, _I, _I]),
+    "bbm_hip_parse_model_tree": (_I, [ctypes.c_char_p, _P, _P, _P, _P, _I, _I]),
+    "bbm_hip_aggregate_eval_pdf_f64": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P]),
+    "bbm_hip_aggregate_sample_f64": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "bbm_hip_aggregate_reflectance_f64": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
+    "bbm_hip_scratch_trim": (_SZ, []),
+    "bbm_hip_scratch_bytes": (_SZ, []),
 }
+
+ABI_VERSION = 8
+AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
 
 
 class Child(ctypes.Structure):
-    """bbm_hip_child (include/bbm_hip.h): one child of a composed aggregate."""
-    _fields_ = [("model_id", ctypes.c_int), ("params", ctypes.c_void_p), ("nparams", ctypes.c_int)]
+    """bbm_hip_child (include/bbm_hip.h): one child of a composed aggregate -- a registry model with its float
+    parameters, or (model_id = AGGREGATE) a nested composed aggregate with its own children."""
+    _fields_ = [("model_id", ctypes.c_int), ("params", ctypes.c_void_p), ("nparams", ctypes.c_int),
+                ("children", ctypes.c_void_p), ("nchildren", ctypes.c_int)]
+
+
+class ChildF64(ctypes.Structure):
+    """bbm_hip_child_f64: the same with double parameters (doubleRGB)."""
+    _fields_ = [("model_id", ctypes.c_int), ("params", ctypes.c_void_p), ("nparams", ctypes.c_int),
+                ("children", ctypes.c_void_p), ("nchildren", ctypes.c_int)]
 
 
 class BackboneError(RuntimeError):
@@ -91,6 +108,9 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(LIB_PATH)
+    if not hasattr(lib, "bbm_hip_abi_version") or lib.bbm_hip_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI {lib.bbm_hip_abi_version() if hasattr(lib, 'bbm_hip_abi_version') else '?'}, "
+                          f"this package needs ABI {ABI_VERSION}: rebuild it")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

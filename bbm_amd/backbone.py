@@ -13,6 +13,7 @@ but every call takes N direction pairs at once instead of one:
 All work runs in libbbm_hip (hand-written gfx950 kernels) on the current torch stream; this
 module only allocates outputs and passes pointers.  There is no CPU fallback.
 """
+import copy
 import ctypes
 import enum
 import re
@@ -480,76 +481,103 @@ def fromString(s):
 bsdf_import = fromString
 
 
+def _copy_model(m):
+    """A copy of a model for an aggregate (aggregatemodel_base copies its children, aggregatemodel.h:34): same
+    class, own parameter vector, and every other attribute shared -- a Merl child keeps the reference to the
+    device table its parameters point to."""
+    if isinstance(m, AggregateModel):
+        return AggregateModel(*m._children)
+    c = copy.copy(m)
+    c._params = m._params.copy()
+    return c
+
+
 class AggregateModel:
-    """aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 models that have kernels
-    of their own (single models or fused aggregates), evaluated by composing the children's kernels
-    (bbm_hip_aggregate_*, bbm_amd/csrc/composite.hip): eval / reflectance = the children's sum (right fold),
-    pdf = their reflectance-weighted mixture, sample = the reference's child selection on xi0.  The published
-    fits' form Aggregate(Lambertian, X) has fused kernels instead (Aggregate(...) picks them).  Parameters are
-    the children's vectors in order (reflection order of the base classes)."""
+    """aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 models -- single models,
+    Merl, fused aggregates, or composed aggregates again (aggregatemodel_base takes any bsdfmodel child, :22) --
+    evaluated by composing the children's kernels (bbm_hip_aggregate_*, bbm_amd/csrc/composite.hip): eval /
+    reflectance = the children's sum (right fold), pdf = their reflectance-weighted mixture, sample = the
+    reference's child selection on xi0; a nested aggregate is one child with its own eval / pdf / sample /
+    reflectance.  The published fits' form Aggregate(Lambertian, X) has fused kernels instead (Aggregate(...)
+    picks them).  Parameters are the children's vectors in order (reflection order of the base classes).
+    float32 tensors evaluate in floatRGB, float64 tensors in doubleRGB (every leaf needs doubleRGB kernels)."""
 
     def __init__(self, *children):
         if len(children) < 2:
             raise ValueError("an aggregate needs at least two child models")
         for c in children:
-            if not isinstance(c, BsdfModel):
-                raise TypeError("aggregate children must be BsdfModel instances with kernels of their own "
-                                "(nested composed aggregates are not supported)")
-        self._children = [BsdfModel(c.name) for c in children]
-        for mine, c in zip(self._children, children):
-            mine._params[:] = c._params
+            if not isinstance(c, (BsdfModel, AggregateModel)):
+                raise TypeError("aggregate children must be models (BsdfModel, Merl or AggregateModel)")
+        self._children = [_copy_model(c) for c in children]
         self.name = aggregate_key([c.name for c in children])
 
     def children(self):
-        out = []
-        for c in self._children:
-            m = BsdfModel(c.name)
-            m._params[:] = c._params
-            out.append(m)
-        return out
+        return [_copy_model(c) for c in self._children]
 
     def parameter_values(self, flag=None):
         return np.concatenate([c.parameter_values(flag) for c in self._children])
 
     def set_parameter_values(self, values):
         v = np.asarray(values, dtype=np.float32).reshape(-1)
-        if v.size != sum(c._params.size for c in self._children):
-            raise ValueError(f"{self.name}: expected {sum(c._params.size for c in self._children)} parameters")
+        sizes = [c.parameter_values().size for c in self._children]
+        if v.size != sum(sizes):
+            raise ValueError(f"{self.name}: expected {sum(sizes)} parameters, got {v.size}")
         k = 0
-        for c in self._children:
-            c._params[:] = v[k:k + c._params.size]
-            k += c._params.size
+        for c, n in zip(self._children, sizes):
+            c.set_parameter_values(v[k:k + n])
+            k += n
 
     def __str__(self):
         return "Aggregate(" + ", ".join(str(c) for c in self._children) + ")"
 
     __repr__ = __str__
 
-    def _desc(self):
-        arr = (_lib.Child * len(self._children))()
-        for a, c in zip(arr, self._children):
-            a.model_id, a.params, a.nparams = c.model_id, c._params.ctypes.data, c._params.size
-        return arr
+    def has_f64(self):
+        return all(c.has_f64() for c in self._children)
+
+    def _desc(self, f64=False):
+        """ctypes bbm_hip_child(_f64) array of the children, nested aggregates as AGGREGATE nodes; returns (array,
+        keep-alive list of the arrays and parameter buffers it points to)."""
+        keep = []
+        kind = _lib.ChildF64 if f64 else _lib.Child
+
+        def build(kids):
+            arr = (kind * len(kids))()
+            keep.append(arr)
+            for a, c in zip(arr, kids):
+                if isinstance(c, AggregateModel):
+                    sub = build(c._children)
+                    a.model_id, a.params, a.nparams = _lib.AGGREGATE, None, 0
+                    a.children, a.nchildren = ctypes.cast(sub, ctypes.c_void_p), len(c._children)
+                else:
+                    c._pptr()          # a Merl child checks its table's device here
+                    p = np.ascontiguousarray(c._params, dtype=np.float64) if f64 else c._params
+                    keep.append(p)
+                    a.model_id, a.params, a.nparams = c.model_id, p.ctypes.data, p.size
+                    a.children, a.nchildren = None, 0
+            return arr
+        return build(self._children), keep
 
     def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
                  rgb=None, pdf=None, stream=None, mode=3):
         torch = _torch()
-        ix, iy, iz, n = _soa(in_, what="in")
-        ox, oy, oz, _ = _soa(out, n, what="out")
+        f64 = _is_f64(in_)
+        dt = torch.float64 if f64 else torch.float32
+        ix, iy, iz, n = _soa(in_, what="in", dtype=dt)
+        ox, oy, oz, _ = _soa(out, n, what="out", dtype=dt)
         mptr, _keep = _mask_ptr(mask, n)
         dev = torch.device("cuda", torch.cuda.current_device())
         if mode & 1:
-            rgb = torch.empty((3, n), dtype=torch.float32, device=dev) if rgb is None else \
-                _out_rows(rgb, 3, n, dev, "rgb")
+            rgb = torch.empty((3, n), dtype=dt, device=dev) if rgb is None else _out_rows(rgb, 3, n, dev, "rgb", dt)
         if mode & 2:
-            pdf = torch.empty((n,), dtype=torch.float32, device=dev) if pdf is None else \
-                _out_rows(pdf, 0, n, dev, "pdf")
+            pdf = torch.empty((n,), dtype=dt, device=dev) if pdf is None else _out_rows(pdf, 0, n, dev, "pdf", dt)
         _on_stream(stream, _keep, rgb, pdf)
-        d = self._desc()
-        _lib.check(_lib.load().bbm_hip_aggregate_eval_pdf(
-            d, len(self._children), ix, iy, iz, ox, oy, oz, mptr, n, int(component), int(unit),
-            rgb[0].data_ptr() if mode & 1 else None, rgb[1].data_ptr() if mode & 1 else None,
-            rgb[2].data_ptr() if mode & 1 else None, pdf.data_ptr() if mode & 2 else None, _stream_ptr(stream)))
+        d, _kd = self._desc(f64)
+        fn = _lib.load().bbm_hip_aggregate_eval_pdf_f64 if f64 else _lib.load().bbm_hip_aggregate_eval_pdf
+        _lib.check(fn(d, len(self._children), ix, iy, iz, ox, oy, oz, mptr, n, int(component), int(unit),
+                      rgb[0].data_ptr() if mode & 1 else None, rgb[1].data_ptr() if mode & 1 else None,
+                      rgb[2].data_ptr() if mode & 1 else None, pdf.data_ptr() if mode & 2 else None,
+                      _stream_ptr(stream)))
         return rgb, pdf
 
     eval = BsdfModel.eval
@@ -557,34 +585,39 @@ class AggregateModel:
 
     def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
         torch = _torch()
-        ox, oy, oz, n = _soa(out, what="out")
+        f64 = _is_f64(out)
+        dt = torch.float64 if f64 else torch.float32
+        ox, oy, oz, n = _soa(out, what="out", dtype=dt)
         x0, x1 = (xi if isinstance(xi, (tuple, list)) else (xi[0], xi[1]))
         for x in (x0, x1):
-            if x.dtype != torch.float32 or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
-                raise TypeError("xi: expected float32 CUDA rows with one entry per direction")
+            if x.dtype != dt or not x.is_cuda or x.numel() != n or x.stride(0) != 1:
+                raise TypeError(f"xi: expected {str(dt).replace('torch.', '')} CUDA rows with one entry per direction")
         mptr, _keep = _mask_ptr(mask, n)
         dev = x0.device
-        d = torch.empty((3, n), dtype=torch.float32, device=dev)
-        p = torch.empty((n,), dtype=torch.float32, device=dev)
+        d = torch.empty((3, n), dtype=dt, device=dev)
+        p = torch.empty((n,), dtype=dt, device=dev)
         f = torch.empty((n,), dtype=torch.int32, device=dev)
         _on_stream(stream, _keep, d, p, f)
-        desc = self._desc()
-        _lib.check(_lib.load().bbm_hip_aggregate_sample(
-            desc, len(self._children), ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component), int(unit),
-            d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(), _stream_ptr(stream)))
+        desc, _kd = self._desc(f64)
+        fn = _lib.load().bbm_hip_aggregate_sample_f64 if f64 else _lib.load().bbm_hip_aggregate_sample
+        _lib.check(fn(desc, len(self._children), ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
+                      int(unit), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
+                      _stream_ptr(stream)))
         return BsdfSample(d, p, f)
 
     def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None):
         torch = _torch()
-        ox, oy, oz, n = _soa(out, what="out")
+        f64 = _is_f64(out)
+        dt = torch.float64 if f64 else torch.float32
+        ox, oy, oz, n = _soa(out, what="out", dtype=dt)
         mptr, _keep = _mask_ptr(mask, n)
         dev = (out[0] if isinstance(out, (tuple, list)) else out).device
-        rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
+        rgb = torch.empty((3, n), dtype=dt, device=dev)
         _on_stream(stream, _keep, rgb)
-        desc = self._desc()
-        _lib.check(_lib.load().bbm_hip_aggregate_reflectance(
-            desc, len(self._children), ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
-            rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
+        desc, _kd = self._desc(f64)
+        fn = _lib.load().bbm_hip_aggregate_reflectance_f64 if f64 else _lib.load().bbm_hip_aggregate_reflectance
+        _lib.check(fn(desc, len(self._children), ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
+                      rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
         return rgb
 
 
@@ -605,6 +638,17 @@ def _make_ctor(name):
     if name in ATTRIBUTES:
         ctor.__doc__ = f"Constructs: {name}({', '.join(a for a, _ in ATTRIBUTES[name])}) -- {nparams(name)} parameters"
     return ctor
+
+
+def scratch_trim():
+    """Return the library's idle device scratch (per-launch temporaries of composed aggregates and tabulated
+    samplers) to the device (bbm_hip_scratch_trim); returns the bytes freed."""
+    return int(_lib.load().bbm_hip_scratch_trim())
+
+
+def scratch_bytes():
+    """Device bytes the library's scratch pool currently holds (bbm_hip_scratch_bytes)."""
+    return int(_lib.load().bbm_hip_scratch_bytes())
 
 
 def fill_directions(seed, stream_id, offset, n, mode=0, out=None, stream=None):

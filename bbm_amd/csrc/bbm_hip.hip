@@ -41,15 +41,51 @@ std::mutex g_scratch_mu;
 std::vector<ScratchBlock> g_scratch;
 }  // namespace
 
+namespace {
+// idle bytes kept for reuse before released blocks are returned to the device (BBM_HIP_SCRATCH_RETAIN_MB)
+size_t retain_limit()
+{
+  static const size_t v = [] {
+    const char* e = std::getenv("BBM_HIP_SCRATCH_RETAIN_MB");
+    return size_t(e ? std::strtoull(e, nullptr, 10) : 1024ull) << 20;
+  }();
+  return v;
+}
+
+// frees idle blocks (caller holds the lock): wait = false only those whose last use has completed on the GPU;
+// wait = true all of them, after their release event.  `keep`: idle bytes that may stay.  Returns bytes freed.
+size_t free_idle(bool wait, size_t keep)
+{
+  size_t idle = 0, freed = 0;
+  for (const ScratchBlock& b : g_scratch) idle += b.busy ? 0 : b.bytes;
+  for (size_t i = g_scratch.size(); i-- > 0 && idle > keep;)
+  {
+    ScratchBlock& b = g_scratch[i];
+    if (b.busy) continue;
+    if (b.used && (wait ? hipEventSynchronize(b.released) : hipEventQuery(b.released)) != hipSuccess) continue;
+    (void)hipFree(b.p);
+    (void)hipEventDestroy(b.released);
+    idle -= b.bytes;
+    freed += b.bytes;
+    g_scratch.erase(g_scratch.begin() + long(i));
+  }
+  return freed;
+}
+}  // namespace
+
 void* scratch_acquire(size_t bytes, hipStream_t s)
 {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   bytes = (bytes + 255) & ~size_t(255);
   std::lock_guard<std::mutex> lock(g_scratch_mu);
+  // best fit among idle blocks of this device, but not one much larger than the request (a 360-byte CDF must not
+  // pin a block sized for 125M lanes)
   ScratchBlock* best = nullptr;
   for (ScratchBlock& b : g_scratch)
-    if (!b.busy && b.device == dev && b.bytes >= bytes && (!best || b.bytes < best->bytes)) best = &b;
+    if (!b.busy && b.device == dev && b.bytes >= bytes && (b.bytes <= 4 * bytes || b.bytes - bytes <= (size_t(1) << 20)) &&
+        (!best || b.bytes < best->bytes))
+      best = &b;
   if (best)
   {
     // its last user's work must be done before this stream writes it: free on the same stream (stream
@@ -59,7 +95,13 @@ void* scratch_acquire(size_t bytes, hipStream_t s)
     return best->p;
   }
   ScratchBlock b{nullptr, bytes, dev, nullptr, s, true, false};
-  if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
+  if (hipMalloc(&b.p, bytes) != hipSuccess)
+  {
+    // out of device memory: return every idle block (after its last use) and try once more
+    (void)hipGetLastError();
+    free_idle(true, 0);
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return nullptr;
+  }
   if (hipEventCreateWithFlags(&b.released, hipEventDisableTiming) != hipSuccess)
   {
     (void)hipFree(b.p);
@@ -79,8 +121,23 @@ void scratch_release(void* p, hipStream_t s)
       b.last = s;
       b.busy = false;
       b.used = true;
-      return;
+      break;
     }
+  free_idle(false, retain_limit());
+}
+
+size_t scratch_trim()
+{
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  return free_idle(true, 0);
+}
+
+size_t scratch_bytes()
+{
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  size_t t = 0;
+  for (const ScratchBlock& b : g_scratch) t += b.bytes;
+  return t;
 }
 
 BBM_HIP_MICROFACET_MODELS(BBM_HIP_EXTERN)
@@ -471,6 +528,10 @@ using namespace bbmhip;
 extern "C" {
 
 int bbm_hip_abi_version(void) { return BBM_HIP_ABI_VERSION; }
+
+size_t bbm_hip_scratch_trim(void) { return scratch_trim(); }
+
+size_t bbm_hip_scratch_bytes(void) { return scratch_bytes(); }
 
 const char* bbm_hip_last_error(void) { return g_last_error.c_str(); }
 

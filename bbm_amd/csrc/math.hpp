@@ -136,6 +136,53 @@ __device__ __forceinline__ float expf_dn(float x)
   return (x < -104.0f) ? 0.0f : ((x > 88.7228394f) ? __builtin_inff() : r);
 }
 
+// expf, branch-free, over the whole float range: the float nearest e^x (what glibc's expf returns, <= 0.502 ulp)
+// except within ~2^-20 ulp of a rounding midpoint, subnormal results rounded once.  t = x log2(e) in double
+// (|t| <= 150 on the finite domain: absolute error <= 2^-45.8) and exp2_cr: ~15 f64 VALU per call against ~10 f32
+// for expf_dn, whose 1.4-ulp results differ from glibc's by an ulp on a few percent of all lanes and by a
+// subnormal ulp -- up to 1e-4 relative once a quotient lifts the value back into the normal range -- below
+// x = -87.3.  Every lane takes the same path, so no divergence (the earlier exact-below-the-normal-range branch
+// cost the headline kernel 9 %).
+__device__ __forceinline__ float expf_rn(float x) { return exp2_cr(double(x) * 1.4426950408889634074); }
+
+// glibc's expf itself (glibc 2.35, sysdeps/ieee754/flt-32/e_expf.c with e_exp2f_data.c -- the Arm
+// optimized-routines algorithm the reference's bbm::exp(float) -> std::exp -> expf runs on x86-64), restated in
+// IEEE double ops: x N / ln2 = k + r (N = 32), 2^(k/N) from a 32-entry table of doubles plus an exponent shift,
+// 2^(r/N) by a cubic, one final rounding to float.  The x86-64 library is the ifunc variant built with FMA
+// contraction (__expf_fma on any FMA-capable host): r = fma(InvLn2N, x, -kd) and the cubic's three FMAs.  This
+// restatement returns the same float as the container's libm for EVERY float in [-110, 90] (2.24e9 inputs,
+// oracle/expf_glibc_check.c); outside that range glibc's special cases (0, inf, NaN) are mirrored by selects.
+// ~10 f64 VALU + a 64-bit table gather, branch-free: cheaper than exp2_cr's polynomial and exact to the bit.
+__device__ __constant__ const uint64_t kExpfTab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+__device__ __forceinline__ float expf_glibc(float x)
+{
+  constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
+  constexpr double kShift = 0x1.8p+52;
+  constexpr double kC0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, kC1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+                   kC2 = 0x1.62e42ff0c52d6p-1 / 32;
+  const double xd = double(x);
+  const double kb = __builtin_fma(kInvLn2N, xd, kShift);          // k in the low bits (ties to even)
+  const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
+  const double kd = kb - kShift;
+  const double r = __builtin_fma(kInvLn2N, xd, -kd);             // x N / ln2 - k, |r| <= 1/2
+  const double s = __builtin_bit_cast(double, kExpfTab[ki & 31u] + (ki << 47));   // 2^(k/N)
+  const double z = __builtin_fma(kC0, r, kC1);
+  const double r2 = r * r;
+  double y = __builtin_fma(kC2, r, 1.0);
+  y = __builtin_fma(z, r2, y);
+  const float res = float(y * s);
+  // |x| >= 88 or NaN in glibc: -inf and x < log(2^-150) -> 0, x > log(2^128) -> inf, NaN -> NaN (via res)
+  return (x < -0x1.9fe368p6f) ? 0.0f : ((x > 0x1.62e42ep6f) ? __builtin_inff() : res);
+}
+
 // a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
 // q = a rm corrected once by the exact remainder -- the correctly rounded quotient (as div_nr) without v_rcp_f32
 __device__ __forceinline__ float div_small(float a, float m, float rm)

@@ -38,7 +38,13 @@ struct Beckmann
   {
     const float c2 = h.z * h.z;
     const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
-    float D = div_nr(expf_dn(div_nr(-sn, c2)), au * av * c2 * c2);
+#if defined(BBM_HIP_BECKMANN_EXP_DN)
+    float D = div_nr(expf_dn(div_nr(-sn, c2)), au * av * c2 * c2);      // A/B: the 1.4-ulp exponential
+#elif defined(BBM_HIP_BECKMANN_EXP_RN)
+    float D = div_nr(expf_rn(div_nr(-sn, c2)), au * av * c2 * c2);      // A/B: correctly rounded
+#else
+    float D = div_nr(expf_glibc(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit
+#endif
     if (Normalize) D *= kInvPiF;
     return (h.z > 0) ? D : 0.0f;
   }

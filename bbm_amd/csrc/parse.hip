@@ -5,8 +5,10 @@
 // used by checkBsdf (bin/checkBsdf.cpp:435-479), the Mitsuba plugin and the .fit files.  bbm_hip_parse_model
 // restates it for the C-ABI: `Name(attr = value, ...)` (attributes by name in any order, or positionally in
 // declaration order; missing ones keep their defaults; a scalar broadcasts over an RGB / Vec2d attribute) and
-// `Aggregate(child, child, ...)`.  A single model or an Aggregate(Lambertian, X) with a fused kernel yields one
-// registry entry; any other aggregate yields its children, for the composed path (bbm_hip_aggregate_*).
+// `Aggregate(child, child, ...)`, nested to any depth.  A single model or an Aggregate(Lambertian, X) with a fused
+// kernel is one registry entry; any other aggregate is a composed node whose children are entries or composed
+// nodes again, for the composed path (bbm_hip_aggregate_*): bbm_hip_parse_model returns one level, and
+// bbm_hip_parse_model_tree the whole tree in preorder.
 // Errors follow the reference's std::invalid_argument cases (unknown name, malformed string, unknown
 // attribute, wrong value count) plus std::out_of_range (a value beyond the float range).
 #include <cctype>
@@ -189,46 +191,64 @@ bool parse_single(Parser& p, const std::string& name, Child& out, int& code)
   return true;
 }
 
-bool parse_any(Parser& p, std::vector<Child>& kids, int& code)
+// A parsed model: a registry entry (single model or fused aggregate) with its parameters, or a composed
+// aggregate (kids.size() >= 2) whose children are nodes again -- aggregatemodel_base takes any bsdfmodel child
+// (aggregatemodel.h:22), including another aggregate, and keeps it as one child: its eval / pdf / sample /
+// reflectance stay the inner aggregate's own (no flattening, which would change the fold order and the sampling).
+struct Node
+{
+  Child leaf;
+  std::vector<Node> kids;
+  bool composed() const { return !kids.empty(); }
+};
+
+bool parse_any(Parser& p, Node& node, int& code)
 {
   const std::string name = p.ident();
   if (name.empty()) { code = BBM_HIP_ERR_INVALID_ARG; p.err = "malformed BSDF string"; return false; }
-  if (name != "Aggregate")
-  {
-    kids.emplace_back();
-    return parse_single(p, name, kids.back(), code);
-  }
+  if (name != "Aggregate") return parse_single(p, name, node.leaf, code);
   if (!p.eat('(')) { code = BBM_HIP_ERR_INVALID_ARG; p.err = "Aggregate: expected '('"; return false; }
-  std::vector<Child> sub;
+  std::vector<Node> sub;
   do
   {
-    if (!parse_any(p, sub, code)) return false;
+    sub.emplace_back();
+    if (!parse_any(p, sub.back(), code)) return false;
   } while (p.eat(','));
   if (!p.eat(')')) { code = BBM_HIP_ERR_INVALID_ARG; p.err = "Aggregate: expected ')'"; return false; }
   if (sub.size() < 2) { code = BBM_HIP_ERR_INVALID_ARG; p.err = "Aggregate: needs at least two models"; return false; }
-  // a fused kernel for exactly this composition (the fits' Aggregate(Lambertian, X))?
+  // a fused kernel for exactly this composition of registry entries (the fits' Aggregate(Lambertian, X))?
+  bool flat = true;
   std::string key = "Aggregate<";
-  for (size_t k = 0; k < sub.size(); ++k) key += (k ? "," : "") + sub[k].name;
+  for (size_t k = 0; k < sub.size(); ++k)
+  {
+    flat = flat && !sub[k].composed();
+    key += (k ? "," : "") + sub[k].leaf.name;
+  }
   key += ">";
-  const int fid = bbm_hip_model_id(key.c_str());
+  const int fid = flat ? bbm_hip_model_id(key.c_str()) : -1;
   if (fid >= 0)
   {
-    Child c;
-    c.name = key;
-    for (const auto& k : sub) c.params.insert(c.params.end(), k.params.begin(), k.params.end());
-    kids.push_back(c);
+    node.leaf.name = key;
+    for (const auto& k : sub) node.leaf.params.insert(node.leaf.params.end(), k.leaf.params.begin(), k.leaf.params.end());
   }
-  else
-  {
-    for (const auto& k : sub)
-      if (k.name.rfind("Aggregate<", 0) == 0)
-      {
-        code = BBM_HIP_ERR_UNSUPPORTED;
-        p.err = "nested aggregate without a fused kernel: " + k.name;
-        return false;
-      }
-    kids.insert(kids.end(), sub.begin(), sub.end());
-  }
+  else node.kids = std::move(sub);
+  return true;
+}
+
+// preorder flattening for bbm_hip_parse_model_tree
+void preorder(const Node& n, std::vector<const Node*>& out)
+{
+  out.push_back(&n);
+  for (const auto& k : n.kids) preorder(k, out);
+}
+
+bool parse_root(const std::string& s, Node& root, int& rc)
+{
+  Parser p(s);
+  int code = BBM_HIP_OK;
+  if (!parse_any(p, root, code)) { rc = fail(code, p.err.empty() ? "malformed BSDF string: " + s : p.err); return false; }
+  p.ws();
+  if (p.i != s.size()) { rc = fail(BBM_HIP_ERR_INVALID_ARG, "malformed BSDF string (trailing text): " + s); return false; }
   return true;
 }
 
@@ -251,25 +271,57 @@ int bbm_hip_parse_model(const char* str, int* model_ids, float* params, int* npa
 {
   if (!str) return fail(BBM_HIP_ERR_INVALID_ARG, "string is NULL");
   const std::string s(str);
-  Parser p(s);
-  std::vector<Child> kids;
-  int code = BBM_HIP_OK;
-  if (!parse_any(p, kids, code)) return fail(code, p.err.empty() ? "malformed BSDF string: " + s : p.err);
-  p.ws();
-  if (p.i != s.size()) return fail(BBM_HIP_ERR_INVALID_ARG, "malformed BSDF string (trailing text): " + s);
+  Node root;
+  int rc = BBM_HIP_OK;
+  if (!parse_root(s, root, rc)) return rc;
+  std::vector<const Child*> kids;
+  if (!root.composed()) kids.push_back(&root.leaf);
+  for (const auto& k : root.kids)
+  {
+    if (k.composed())
+      return fail(BBM_HIP_ERR_UNSUPPORTED, "a composed aggregate nested in another: use bbm_hip_parse_model_tree (" + s + ")");
+    kids.push_back(&k.leaf);
+  }
   if (int(kids.size()) > max_children)
     return fail(BBM_HIP_ERR_INVALID_ARG, "too many children for the output arrays (" + std::to_string(kids.size()) + ")");
   int total = 0;
-  for (const auto& k : kids) total += int(k.params.size());
+  for (const Child* k : kids) total += int(k->params.size());
   if (total > params_capacity) return fail(BBM_HIP_ERR_INVALID_ARG, "params capacity too small (" + std::to_string(total) + ")");
   int off = 0;
   for (size_t c = 0; c < kids.size(); ++c)
   {
-    if (model_ids) model_ids[c] = bbm_hip_model_id(kids[c].name.c_str());
-    if (nparams) nparams[c] = int(kids[c].params.size());
-    for (float v : kids[c].params) if (params) params[off++] = v;
+    if (model_ids) model_ids[c] = bbm_hip_model_id(kids[c]->name.c_str());
+    if (nparams) nparams[c] = int(kids[c]->params.size());
+    for (float v : kids[c]->params) if (params) params[off++] = v;
   }
   return int(kids.size());
+}
+
+int bbm_hip_parse_model_tree(const char* str, int* model_ids, int* nchildren, float* params, int* nparams,
+                             int max_nodes, int params_capacity)
+{
+  if (!str) return fail(BBM_HIP_ERR_INVALID_ARG, "string is NULL");
+  const std::string s(str);
+  Node root;
+  int rc = BBM_HIP_OK;
+  if (!parse_root(s, root, rc)) return rc;
+  std::vector<const Node*> nodes;
+  preorder(root, nodes);
+  if (int(nodes.size()) > max_nodes)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "too many nodes for the output arrays (" + std::to_string(nodes.size()) + ")");
+  int total = 0;
+  for (const Node* n : nodes) total += int(n->leaf.params.size());
+  if (total > params_capacity) return fail(BBM_HIP_ERR_INVALID_ARG, "params capacity too small (" + std::to_string(total) + ")");
+  int off = 0;
+  for (size_t k = 0; k < nodes.size(); ++k)
+  {
+    const Node& n = *nodes[k];
+    if (model_ids) model_ids[k] = n.composed() ? BBM_HIP_AGGREGATE : bbm_hip_model_id(n.leaf.name.c_str());
+    if (nchildren) nchildren[k] = int(n.kids.size());
+    if (nparams) nparams[k] = int(n.leaf.params.size());
+    for (float v : n.leaf.params) if (params) params[off++] = v;
+  }
+  return int(nodes.size());
 }
 
 }  // extern "C"

@@ -67,6 +67,13 @@ def parse(argv=None):
                                                    "(counter passes profile one model at a time)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="evalpdf: time the K steps as HIP-graph replays of R launches (K/R replays, R | K) instead of "
+                         "one Python-side launch per step; auto = when this rank's shard is below --graph-below pairs "
+                         "(a ~0.2 ms kernel, e.g. 12.5M pairs per GPU under --scaling strong on 8 GPUs). Both figures "
+                         "are reported; value is the graph-timed one when the graph is used")
+    ap.add_argument("--graph-below", type=int, default=30_000_000)
+    ap.add_argument("--fit-max-steps", type=int, default=3000, help="fit: compass steps cap for the convergence run")
     ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "f64", "selftest"],
                     help="evalpdf: the BASELINE metric (config 2, default); models: every model's eval over shared "
                          "pairs (config 3); sample: importance-sample -> eval -> pdf MC loop (config 4); fit: "
@@ -111,10 +118,20 @@ def cpu_baseline(model, din, dout, seconds):
 
 
 def selftest(args, dist, rank, world):
-    """Harness only: a trivial CPU step under the same launch / barrier / max-over-ranks timing."""
+    """Harness only: a trivial CPU step under the same launch / barrier / max-over-ranks timing, with the evalpdf
+    workload's --graph choice (a 'graph' here is R steps issued by one call, R = bh.graph_reps(K))."""
     begin, n = bh.shard(args.pairs, rank, world, args.scaling)
     x = torch.arange(n, dtype=torch.float32)
     elapsed, _, per_rank, settle = bh.timed(lambda: x.sum(), args, dist, gpu=False)
+    use_graph = args.graph == "on" or (args.graph == "auto" and n < args.graph_below)
+    timing = {"launch_timed": {"elapsed_s": elapsed, "rank_ms_per_step": [t * 1e3 / args.steps for t in per_rank]}}
+    if use_graph:
+        reps = bh.graph_reps(args.steps)
+        g_el, _, g_per, _ = bh.timed(lambda: [x.sum() for _ in range(reps)],
+                                     argparse.Namespace(**{**vars(args), "steps": args.steps // reps}), dist, gpu=False)
+        timing["graph_timed"] = {"elapsed_s": g_el, "launches_per_replay": reps, "replays": args.steps // reps,
+                                 "rank_ms_per_step": [t * 1e3 / args.steps for t in g_per]}
+        elapsed, per_rank = g_el, g_per
     if rank == 0:
         total = (n * world if args.scaling == "weak" else args.pairs) * args.steps
         print(json.dumps({"metric": "bench harness self-test (CPU, no BSDF work)", "value": total / elapsed,
@@ -124,7 +141,9 @@ def selftest(args, dist, rank, world):
                           "config": {"workload": "selftest", "units_per_rank": n,
                                      "parallelism": f"dp{world}"},
                           "ranks_seen": dist.get_world_size() if dist else 1,
-                          "rank_ms_per_step": [t * 1e3 / args.steps for t in per_rank]}), flush=True)
+                          "rank_ms_per_step": [t * 1e3 / args.steps for t in per_rank],
+                          "timing": dict(timing, value_from="graph_timed" if use_graph else "launch_timed")}),
+              flush=True)
 
 
 def main(argv=None):
@@ -160,8 +179,21 @@ def main(argv=None):
     pdf = torch.empty((n,), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream()
 
-    elapsed, kern_ms, per_rank, settle = bh.timed(
-        lambda: model.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=stream), args, dist, stream)
+    launch = lambda s=stream: model.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=s)   # noqa: E731
+    elapsed, kern_ms, per_rank, settle = bh.timed(launch, args, dist, stream)
+    use_graph = args.graph == "on" or (args.graph == "auto" and n < args.graph_below)
+    timing = {"launch_timed": {"elapsed_s": elapsed, "kernel_ms": kern_ms, "rank_ms_per_step":
+                               [t * 1e3 / args.steps for t in per_rank]}}
+    if use_graph:
+        # the same K steps as R-launch graph replays: the host issues one replay per R steps
+        reps = bh.graph_reps(args.steps)
+        graph = bh.capture(launch, reps)
+        g_el, g_ms, g_per, _ = bh.timed(graph.replay, argparse.Namespace(**{**vars(args), "steps": args.steps // reps,
+                                                                             "warmup": 2, "settle_s": 0.1}), dist, stream)
+        timing["graph_timed"] = {"elapsed_s": g_el, "kernel_ms": g_ms / reps, "launches_per_replay": reps,
+                                 "replays": args.steps // reps,
+                                 "rank_ms_per_step": [t * 1e3 / args.steps for t in g_per]}
+        elapsed, kern_ms, per_rank = g_el, g_ms / reps, g_per
 
     # sanity: outputs finite and non-trivial
     ok = bool(torch.isfinite(pdf).all()) and float(rgb[0].abs().max()) > 0
@@ -202,6 +234,7 @@ def main(argv=None):
                          "bytes_per_pair": bpp},
             "ranks_seen": dist.get_world_size() if dist else 1,
             "rank_ms_per_step": [t * 1e3 / args.steps for t in per_rank],
+            "timing": dict(timing, value_from="graph_timed" if use_graph else "launch_timed"),
             "outputs_ok": ok,
             "settle": {"seconds": args.settle_s, "extra_untimed_steps": settle},
         }

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 7
+#define BBM_HIP_ABI_VERSION 8
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -141,18 +141,24 @@ int bbm_hip_reflectance_f64(int model_id, const double* params, int nparams,
 
 /* ---------------------------------------------------------------- aggregates of any models */
 
-/* aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 registered models, each
- * child given as (model id, its parameter vector): replaces the reference's variadic template instantiation
- * (aggregatemodel.h:222 `aggregatemodel<MODELS...>`, aggregate() :232-233) for compositions that have no fused
- * registry entry ("Aggregate<Lambertian,X>").  Evaluated by composing the children's kernels (one pass per
- * child; eval and reflectance as the reference's right fold, pdf as the reflectance-weighted mixture, sample
- * by the reference's child selection on xi0).  Same conventions as the single-model entry points; `r` may be
- * NULL in bbm_hip_aggregate_eval_pdf for pdf only, `pdf` NULL for eval only. */
+/* aggregatemodel<MODELS...> (include/bsdfmodel/aggregatemodel.h:22-222) of any >= 2 models, each child given as
+ * (model id, its parameter vector): replaces the reference's variadic template instantiation (aggregatemodel.h:222
+ * `aggregatemodel<MODELS...>`, aggregate() :232-233) for compositions that have no fused registry entry
+ * ("Aggregate<Lambertian,X>").  A child may itself be a composed aggregate (the reference's aggregatemodel_base
+ * takes any bsdfmodel child, :22, including another aggregate): model_id = BBM_HIP_AGGREGATE, params unused, and
+ * its own children in `children` / `nchildren` (any depth).  Evaluated by composing the children's kernels (one
+ * pass per child; eval and reflectance as the reference's right fold, pdf as the reflectance-weighted mixture,
+ * sample by the reference's child selection on xi0, each nested aggregate exactly as its own aggregatemodel
+ * member functions would).  Same conventions as the single-model entry points; `r` may be NULL in
+ * bbm_hip_aggregate_eval_pdf for pdf only, `pdf` NULL for eval only. */
+#define BBM_HIP_AGGREGATE (-100)
 typedef struct bbm_hip_child
 {
-  int model_id;
-  const float* params;   /* host memory, nparams floats (bbm_hip_model_nparams) */
-  int nparams;
+  int model_id;                            /* registry id, or BBM_HIP_AGGREGATE */
+  const float* params;                     /* host memory, nparams floats (bbm_hip_model_nparams); aggregate: NULL */
+  int nparams;                             /* aggregate: 0 */
+  const struct bbm_hip_child* children;    /* BBM_HIP_AGGREGATE: its children; else NULL */
+  int nchildren;                           /* BBM_HIP_AGGREGATE: >= 2; else 0 */
 } bbm_hip_child;
 
 int bbm_hip_aggregate_eval_pdf(const bbm_hip_child* children, int nchildren,
@@ -170,6 +176,33 @@ int bbm_hip_aggregate_reflectance(const bbm_hip_child* children, int nchildren,
                                   const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
                                   float* r, float* g, float* b, void* stream);
 
+/* The same in doubleRGB (Value = double): every leaf must have doubleRGB kernels (bbm_hip_model_has_f64); the
+ * combining arithmetic (folds, weights, mixture, child selection) is the reference's in double. */
+typedef struct bbm_hip_child_f64
+{
+  int model_id;
+  const double* params;
+  int nparams;
+  const struct bbm_hip_child_f64* children;
+  int nchildren;
+} bbm_hip_child_f64;
+
+int bbm_hip_aggregate_eval_pdf_f64(const bbm_hip_child_f64* children, int nchildren,
+                                   const double* in_x, const double* in_y, const double* in_z,
+                                   const double* out_x, const double* out_y, const double* out_z,
+                                   const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                                   double* r, double* g, double* b, double* pdf, void* stream);
+int bbm_hip_aggregate_sample_f64(const bbm_hip_child_f64* children, int nchildren,
+                                 const double* out_x, const double* out_y, const double* out_z,
+                                 const double* xi0, const double* xi1,
+                                 const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                                 double* dir_x, double* dir_y, double* dir_z, double* pdf, uint32_t* flag,
+                                 void* stream);
+int bbm_hip_aggregate_reflectance_f64(const bbm_hip_child_f64* children, int nchildren,
+                                      const double* out_x, const double* out_y, const double* out_z,
+                                      const uint8_t* mask, size_t n, uint32_t component, uint32_t unit,
+                                      double* r, double* g, double* b, void* stream);
+
 /* ---------------------------------------------------------------- model strings */
 
 /* Attribute layout of a single model, "name:count,..." in declaration order (the order of its parameter
@@ -180,10 +213,29 @@ const char* bbm_hip_model_layout(int model_id);
  * reference's runtime fromString does (include/bbm/bsdf_string_convert.h:52-85; the handle behind bsdf_ptr,
  * checkBsdf and the Mitsuba plugin).  A single model or an aggregate with a fused kernel yields ONE entry
  * (model_ids[0], its nparams[0] parameters); any other aggregate yields one entry per child, to be evaluated
- * with bbm_hip_aggregate_*.  Parameters are written back to back into params.  Returns the number of entries
- * (>= 1) or an error code (unknown model / attribute, malformed string, value beyond the float range). */
+ * with bbm_hip_aggregate_* (a child may be a fused aggregate).  Parameters are written back to back into params.
+ * Returns the number of entries (>= 1) or an error code (unknown model / attribute, malformed string, value beyond
+ * the float range; BBM_HIP_ERR_UNSUPPORTED for a composed aggregate nested inside another: use
+ * bbm_hip_parse_model_tree). */
 int bbm_hip_parse_model(const char* str, int* model_ids, float* params, int* nparams, int max_children,
                         int params_capacity);
+
+/* The same for any nesting, as a tree in preorder: node k is model_ids[k] (a registry id, or BBM_HIP_AGGREGATE
+ * for a composed aggregate, whose nchildren[k] >= 2 children follow it in preorder; 0 for a registry model) with
+ * nparams[k] parameters (0 for BBM_HIP_AGGREGATE) written back to back into params.  A string without a composed
+ * aggregate gives one node.  Returns the node count or an error code. */
+int bbm_hip_parse_model_tree(const char* str, int* model_ids, int* nchildren, float* params, int* nparams,
+                             int max_nodes, int params_capacity);
+
+/* ---------------------------------------------------------------- device scratch */
+
+/* Return every idle block of the library's stream-ordered scratch pool (per-launch temporaries: sampler CDFs,
+ * composed aggregates' per-lane terms) to the device, after the work that last used it has completed.  The pool
+ * also frees idle blocks by itself beyond BBM_HIP_SCRATCH_RETAIN_MB (default 1024) of retained memory and when
+ * an allocation fails.  Returns the bytes freed. */
+size_t bbm_hip_scratch_trim(void);
+/* Bytes the pool currently holds (idle + in use). */
+size_t bbm_hip_scratch_bytes(void);
 
 /* ---------------------------------------------------------------- fitting (BASELINE config 5) */
 

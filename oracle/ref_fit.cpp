@@ -74,6 +74,19 @@ struct aggv
          &ops<typename aggv<__VA_ARGS__>::d>::template sample<double>, \
          &ops<typename aggv<__VA_ARGS__>::d>::template evalpdf<double, double> }
 
+// an aggregate given by its floatRGB and doubleRGB types (nested aggregates: aggregatemodel_base takes any
+// bsdfmodel child, aggregatemodel.h:22)
+#define BBMREF_AGGT(KEY, TF, TD) \
+  entry{ KEY, &ops<TF>::defaults, &ops<TF>::bounds, &ops<TF>::to_string, &ops<TF>::template evalpdf<float>, \
+         &ops<TD>::template evalpdf<double>, &ops<TF>::template sample<float>, &ops<TF>::template reflectance<float>, \
+         &ops<TF>::from_string, &ops<TD>::template reflectance<double>, &ops<TD>::template sample<double>, \
+         &ops<TD>::template evalpdf<double, double> }
+
+template<typename T> using nested1_t = bbm::aggregatemodel<bbm::aggregatemodel<bbm::lambertian<T>, bbm::ward<T>>, bbm::ggx<T>>;
+template<typename T> using nested2_t = bbm::aggregatemodel<bbm::aggregatemodel<bbm::lambertian<T>, bbm::cooktorrance<T>>, bbm::ward<T>>;
+template<typename T>
+using nested3_t = bbm::aggregatemodel<bbm::ggx<T>, bbm::aggregatemodel<bbm::phong<T>, bbm::aggregatemodel<bbm::ward<T>, bbm::orennayar<T>>>>;
+
 #define BBMREF_AGG(X, KEY) \
   entry{ KEY, \
          &ops<agg<X>>::defaults, &ops<agg<X>>::bounds, &ops<agg<X>>::to_string, \
@@ -102,6 +115,9 @@ const std::vector<entry>& aggregate_registry()
     BBMREF_AGGV("Aggregate<Lambertian,CookTorrance,GGX>", lambertian_t, cooktorrance_t, ggx_t),
     BBMREF_AGGV("Aggregate<CookTorrance,GGX>", cooktorrance_t, ggx_t),
     BBMREF_AGGV("Aggregate<OrenNayar,NganHe,Ward>", orennayar_t, nganhe_t, ward_t),
+    BBMREF_AGGT("Aggregate<Aggregate<Lambertian,Ward>,GGX>", nested1_t<C>, nested1_t<CD>),
+    BBMREF_AGGT("Aggregate<Aggregate<Lambertian,CookTorrance>,Ward>", nested2_t<C>, nested2_t<CD>),
+    BBMREF_AGGT("Aggregate<GGX,Aggregate<Phong,Aggregate<Ward,OrenNayar>>>", nested3_t<C>, nested3_t<CD>),
   };
   return r;
 }

@@ -65,6 +65,48 @@ template<typename CONF>
 using epd = bbm::microfacet<bbm::ndf::epd<CONF>, bbm::maskingshadowing::vanginneken<CONF>, bbm::fresnel::complex<CONF>,
                             bbm::microfacet_n::Walter, "EPD">;
 
+// aggregatemodel_base<NAME, X...> and the ones with an aggregate child: the reference cannot reflect a nested
+// aggregate as a whole (util/reflection.h:247 needs a reflection_base aggregatemodel_base does not declare), so its
+// parameter vector is its children's, in base-class order -- the layout bbm_hip's composed aggregates use
+template<typename M> struct is_agg : std::false_type {};
+template<auto NM, typename... X>
+struct is_agg<bbm::aggregatemodel_base<NM, X...>> : std::true_type { using kids = std::tuple<X...>; };
+template<typename M> struct nested_agg : std::false_type {};
+template<auto NM, typename... X>
+struct nested_agg<bbm::aggregatemodel_base<NM, X...>> : std::bool_constant<(is_agg<X>::value || ...)> {};
+
+template<typename M>
+std::vector<typename M::Value*> flat_refs(M& m)
+{
+  std::vector<typename M::Value*> r;
+  if constexpr (nested_agg<M>::value)
+    [&]<typename... X>(const std::tuple<X...>*) {
+      ([&] { auto c = flat_refs(static_cast<X&>(m)); r.insert(r.end(), c.begin(), c.end()); }(), ...);
+    }(static_cast<const typename is_agg<M>::kids*>(nullptr));
+  else
+  {
+    auto pv = bbm::parameter_values(m, kAllParams);
+    for(size_t i = 0; i < pv.size(); ++i) { typename M::Value& v = pv[i]; r.push_back(&v); }
+  }
+  return r;
+}
+
+template<typename M>
+std::vector<float> flat_bounds(const M& m, bool upper)
+{
+  std::vector<float> r;
+  if constexpr (nested_agg<M>::value)
+    [&]<typename... X>(const std::tuple<X...>*) {
+      ([&] { auto c = flat_bounds(static_cast<const X&>(m), upper); r.insert(r.end(), c.begin(), c.end()); }(), ...);
+    }(static_cast<const typename is_agg<M>::kids*>(nullptr));
+  else
+  {
+    auto b = upper ? bbm::parameter_upper_bound(m, kAllParams) : bbm::parameter_lower_bound(m, kAllParams);
+    for(auto& v : b) r.push_back(float(v));
+  }
+  return r;
+}
+
 template<typename M>
 struct ops
 {
@@ -76,25 +118,22 @@ struct ops
   {
     M m;
     std::vector<float> r;
-    for(auto& v : bbm::parameter_values(m, kAllParams)) r.push_back(float(v));
+    for(Value* v : flat_refs(m)) r.push_back(float(*v));
     return r;
   }
 
   static M make(const float* p, int np)
   {
     M m;
-    auto pv = bbm::parameter_values(m, kAllParams);
-    for(size_t i = 0; i < pv.size() && int(i) < np; ++i) pv[i] = Value(p[i]);
+    auto pv = flat_refs(m);
+    for(size_t i = 0; i < pv.size() && int(i) < np; ++i) *pv[i] = Value(p[i]);
     return m;
   }
 
   static std::vector<float> bounds(bool upper)
   {
     M m;
-    std::vector<float> r;
-    auto b = upper ? bbm::parameter_upper_bound(m, kAllParams) : bbm::parameter_lower_bound(m, kAllParams);
-    for(auto& v : b) r.push_back(float(v));
-    return r;
+    return flat_bounds(m, upper);
   }
 
   // bbm::fromString<M> (include/bbm/bsdf_string_convert.h, aggregatemodel.h:193-218) -> the parameter vector
@@ -103,9 +142,8 @@ struct ops
     try
     {
       M m = bbm::fromString<M>(std::string(str));
-      auto pv = bbm::parameter_values(m, kAllParams);
       int k = 0;
-      for(auto& v : pv) { if(k < cap) out[k] = float(v); ++k; }
+      for(Value* v : flat_refs(m)) { if(k < cap) out[k] = float(*v); ++k; }
       return k;
     }
     catch(const std::exception&) { return -1; }

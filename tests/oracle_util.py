@@ -181,6 +181,36 @@ def ref_reflectance_double(name, params, dout, component=3, unit=0):
     return res
 
 
+def ref_default_params(name):
+    """The reference's default parameter vector of model `name` (All | Dependent, declaration order; nested
+    aggregates child by child)."""
+    lib = ref()
+    buf = np.zeros(256, np.float32)
+    k = lib.bbmref_default_params(name.encode(), _fp(buf), 256)
+    if k < 0:
+        raise KeyError(f"oracle has no model {name}")
+    return buf[:k].copy()
+
+
+def ref_to_string(name, params):
+    """bbm::toString of model `name` at `params`, from the reference."""
+    lib = ref()
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    buf = ctypes.create_string_buffer(16384)
+    k = lib.bbmref_to_string(name.encode(), _fp(params), params.size, buf, 16384)
+    if k < 0:
+        raise KeyError(f"oracle has no model {name}")
+    return buf.value.decode()
+
+
+def ref_from_string(name, s):
+    """bbm::fromString<name>(s) -> the parameter vector, or None if the reference rejects the string."""
+    lib = ref()
+    buf = np.zeros(256, np.float32)
+    k = lib.bbmref_from_string(name.encode(), s.encode(), _fp(buf), 256)
+    return None if k < 0 else buf[:k].copy()
+
+
 def oracle_models():
     """Models a CPU checker can evaluate on arbitrary inputs: the reference shim if it is present
     (prebuilt in the build container, travels with the tree), else the C restatement."""

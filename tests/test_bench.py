@@ -42,6 +42,33 @@ def test_launcher_two_ranks_one_json_line(scaling):
     assert abs(d["ms_per_step"] - max(d["rank_ms_per_step"])) <= 1e-9 * d["ms_per_step"] + 1e-12
 
 
+@pytest.mark.parametrize("graph", ["on", "off"])
+def test_strong_scaling_two_ranks_graph_flag(graph):
+    """--scaling strong on 2 ranks with the graph-replay timing the evalpdf workload uses for short kernels: both
+    figures reported, value from the graph-timed one, exactly K steps timed as K/R replays of R launches."""
+    r = _run(["--gpus", "2", "--workload", "selftest", "--steps", "12", "--warmup", "1", "--settle-s", "0",
+              "--pairs", "2000", "--scaling", "strong", "--graph", graph])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _lines(r.stdout)[0]
+    assert d["ranks_seen"] == 2 and d["scaling"] == "strong"
+    t = d["timing"]
+    assert "launch_timed" in t and len(t["launch_timed"]["rank_ms_per_step"]) == 2
+    if graph == "on":
+        g = t["graph_timed"]
+        assert t["value_from"] == "graph_timed" and g["launches_per_replay"] * g["replays"] == 12
+        assert g["launches_per_replay"] == bh.graph_reps(12) == 12
+        assert abs(d["ms_per_step"] - max(g["rank_ms_per_step"])) <= 1e-9 * d["ms_per_step"] + 1e-12
+    else:
+        assert t["value_from"] == "launch_timed" and "graph_timed" not in t
+    assert abs(d["value"] * d["ms_per_step"] * 12 / 1e3 - 2000 * 12) <= 1e-6 * 2000 * 12
+
+
+def test_graph_reps_divides_steps():
+    for k in (1, 7, 12, 20, 50, 97, 100):
+        r = bh.graph_reps(k)
+        assert k % r == 0 and 1 <= r <= 20
+
+
 def test_launcher_single_rank_default():
     r = _run(["--workload", "selftest", "--steps", "2", "--warmup", "0", "--settle-s", "0", "--pairs", "10"])
     assert r.returncode == 0, r.stderr[-2000:]

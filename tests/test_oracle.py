@@ -140,3 +140,17 @@ def test_config1_lambertian_native_cpu_1m_pairs():
     want = np.where(up, (albedo[:, None] / np.float32(np.pi)).astype(np.float32), np.float32(0))
     np.testing.assert_array_equal(got[:3], want)
     assert el < 60, el
+
+
+def test_expf_restatement_matches_host_libm():
+    """bbm_amd/csrc/math.hpp expf_glibc restates glibc's expf (the reference's bbm::exp(float) on x86-64);
+    oracle/expf_glibc_check runs the same double steps in C against this host's libm on every 61st float of
+    [-110, 90] (the full sweep, stride 1, is 2.24e9 floats and 0 mismatches -- DESIGN.md §4.2)."""
+    import os
+    import subprocess
+    exe = os.path.join(ou.ROOT, "oracle", "_port", "expf_glibc_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ou.ROOT, "oracle"), "expf"], check=True, capture_output=True)
+    r = subprocess.run([exe, "61"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert " 0 mismatches" in r.stdout

@@ -109,11 +109,19 @@ def _graph(launch, reps):
     return g
 
 
+MODEL_SETS = 4
+
+
 def bench_models(args, dist, rank, world):
+    """Config 3.  Every model's eval over 10M pairs per GPU, timed as HIP-graph replays of GRAPH_REPS launches that
+    cycle over MODEL_SETS distinct input/output sets (360 MB each, 1.44 GB in all): no launch finds its operands in
+    the 256 MiB Infinity Cache left behind by the previous one, so the HBM fractions are HBM measurements."""
     n = 10_000_000
-    din = bbm_amd.fill_directions(SEED, 0, rank * n, n, mode=0)
-    dout = bbm_amd.fill_directions(SEED, 1, rank * n, n, mode=0)
-    rgb = torch.empty((3, n), dtype=torch.float32, device="cuda")
+    sets = []
+    for k in range(MODEL_SETS):
+        sets.append((bbm_amd.fill_directions(SEED + k, 0, rank * n, n, mode=0),
+                     bbm_amd.fill_directions(SEED + k, 1, rank * n, n, mode=0),
+                     torch.empty((3, n), dtype=torch.float32, device="cuda")))
     stream = torch.cuda.current_stream()
     per = {}
     total_t = 0.0
@@ -122,8 +130,14 @@ def bench_models(args, dist, rank, world):
     for name in names:
         m = _merl_from(bbm_amd.CookTorrance()) if name == "Merl" else bbm_amd.BsdfModel(name)
         # one step = a HIP graph of `reps` back-to-back launches: a 10M-pair eval of the HBM-bound models takes
-        # ~35 us, less than one Python-side launch, so per-launch stepping would time the host, not the kernel
-        graph = _graph(lambda s: m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=s), reps)
+        # ~50 us, less than one Python-side launch, so per-launch stepping would time the host, not the kernel
+        cyc = [0]
+
+        def launch(s):
+            din, dout, rgb = sets[cyc[0] % MODEL_SETS]
+            cyc[0] += 1
+            m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=s)
+        graph = _graph(launch, reps)
         elapsed, step_ms = _timed(graph.replay, args, dist, stream)
         kern_ms = step_ms / reps
         bpp = 20 if name in Z_ONLY else 36
@@ -134,9 +148,10 @@ def bench_models(args, dist, rank, world):
     if rank == 0:
         _line(args, world, "BSDF evals/s (eval), all single bsdfmodels, 10M shared pairs per GPU (config 3)",
               len(names) * n * world * args.steps / total_t, "pairs/s", total_t / len(names),
-              {"workload": f"{len(names)} models x eval over {n} shared pairs per GPU, one kernel per model "
-                           f"(replayed as a graph of {reps} launches per step)",
-               "pairs_per_gpu": n, "parallelism": f"dp{world} (independent shards)"},
+              {"workload": f"{len(names)} models x eval over {n} pairs per GPU, one kernel per model (replayed as a "
+                           f"graph of {reps} launches per step over {MODEL_SETS} distinct input/output sets, "
+                           f"{MODEL_SETS * 36 * n / 1e9:.2f} GB > the 256 MiB Infinity Cache)",
+               "pairs_per_gpu": n, "operand_sets": MODEL_SETS, "parallelism": f"dp{world} (independent shards)"},
               {"scaling": "weak", "per_model": per})
 
 
@@ -192,15 +207,33 @@ def _merl_from(source):
         return bbm_amd.Merl(path)
 
 
+FIT_MATERIAL = ("bagher_sgd.fit", "alum-bronze")     # fits/bagher_sgd.fit:3, SURVEY §8(d) C5
+
+
+def fit_material():
+    """(name, model string) of the config-5 material: the reference's published Bagher fit fits/bagher_sgd.fit:3,
+    as committed in tests/golden/fits.json (the reference's fromString of every fits/ line, oracle/gen_golden.py)."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "fits.json")
+    with open(path) as f:
+        rows = json.load(f)[FIT_MATERIAL[0]]
+    for row in rows:
+        if row[0] == FIT_MATERIAL[1]:
+            return row[0], row[1]
+    raise KeyError(FIT_MATERIAL)
+
+
 def bench_fit(args, dist, rank, world):
+    """Config 5.  The measured reference is the published fit fits/bagher_sgd.fit:3 (alum-bronze) written at the
+    MERL bin centres into a MERL-format .binary and read back through bbm_amd.Merl, as a real MERL file would be;
+    the fitted model is Aggregate(Lambertian, Bagher) at its defaults.  value: probe-pair evaluations/s of a
+    compass step's 2P probes (one bbm_hip_loss launch + the RCCL all-reduce), K timed steps; then the compass
+    search runs from the defaults to convergence (compass.h:82-140, step size < eps) or --fit-max-steps, and the
+    line reports its steps, wall time per step and the loss before / after."""
     name = "Aggregate<Lambertian,Bagher>"
+    mat, mstr = fit_material()
     fitted = bbm_amd.BsdfModel(name)
     lin = fit.merl_linearizer()
-    # the measured reference: a MERL-format .binary (no measured data ships with the reference repo) holding a
-    # perturbed Bagher fit at the MERL bin centres, read back through bbm_amd.Merl like a real MERL file
-    source = bbm_amd.BsdfModel(name)
-    source.set_parameter_values((source.parameter_values() * np.float32(1.1)).astype(np.float32))
-    reference = _merl_from(source)
+    reference = _merl_from(bbm_amd.fromString(mstr))
     loss = fit.SampledLoss(fitted, reference, "standardLog", lin, dist=dist)
     idx = fitted.parameter_indices(fit.ALL)
     probes = np.repeat(fitted.parameter_values()[None], 2 * len(idx), axis=0)
@@ -209,17 +242,33 @@ def bench_fit(args, dist, rank, world):
         probes[2 * k + 1, j] *= np.float32(0.99)
     stream = torch.cuda.current_stream()
     elapsed, kern_ms = _timed(lambda: loss.probe_sums(probes), args, dist, stream)
+    # the fit itself, from the defaults
+    comp = fit.Compass(loss)
+    loss0 = float(comp.loss_value)
+    t0 = time.perf_counter()
+    steps = 0
+    while not comp.is_converged() and steps < args.fit_max_steps:
+        comp.step()
+        steps += 1
+    torch.cuda.synchronize()
+    fit_s = time.perf_counter() - t0
     if rank == 0:
         pairs = lin.size()
         _line(args, world, "fitting-loss probe-pair evals/s, Aggregate(Lambertian, Bagher), MERL grid, 2P probes per "
               "compass step (config 5)", len(probes) * pairs * args.steps / elapsed, "probe-pairs/s", elapsed,
               {"workload": f"{len(probes)} probes x {pairs} MERL pairs per compass step (standardLog), sharded grid; "
-                           "reference = Merl model read from a synthetic MERL .binary",
+                           f"reference = Merl model read from a MERL .binary holding fits/{FIT_MATERIAL[0]} "
+                           f"'{mat}' (line 3) at the MERL bin centres",
+               "material": f"fits/{FIT_MATERIAL[0]}:3 {mat}",
                "probes": len(probes), "pairs": pairs, "parallelism": f"dp{world} (grid shards, all-reduce of "
                                                                       f"{len(probes)} doubles per step)"},
               {"scaling": "strong", "compass_steps_per_s": args.steps / elapsed, "kernel_ms": kern_ms,
                "probe_pairs_per_dispatch": len(probes) * (pairs // world),
-               "roofline": valu_roofline("fit:Aggregate", kern_ms, len(probes) * (pairs // world))})
+               "roofline": valu_roofline("fit:Aggregate", kern_ms, len(probes) * (pairs // world)),
+               "fit": {"from": "Aggregate<Lambertian,Bagher> defaults", "steps": steps,
+                       "converged": comp.is_converged(), "max_steps": args.fit_max_steps, "seconds": fit_s,
+                       "ms_per_compass_step": fit_s * 1e3 / max(steps, 1), "loss_start": loss0,
+                       "loss_end": float(comp.loss_value), "final_step_size": float(comp.step_size)}})
 
 
 def bench_f64(args, dist, rank, world):

@@ -119,6 +119,30 @@ def timed(step, args, dist, stream=None, gpu=True):
     return elapsed, kern_ms, per_rank, settle
 
 
+def graph_reps(steps, cap=20):
+    """R = the largest divisor of K (= steps) not above `cap`: K/R replays of an R-launch graph time exactly K steps."""
+    return max(r for r in range(1, min(cap, max(steps, 1)) + 1) if steps % r == 0)
+
+
+def capture(launch, reps):
+    """A HIP graph of `reps` calls of launch(stream), captured on a side stream after one warm-up call (first-use
+    host work happens outside the capture)."""
+    import torch
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        launch(side)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream()
+        for _ in range(reps):
+            launch(s)
+    torch.cuda.synchronize()
+    return g
+
+
 def cpu_topology():
     """(affinity threads, physical cores among them, SMT threads per core, cgroup CPU quota or None, model)."""
     aff = sorted(os.sched_getaffinity(0))

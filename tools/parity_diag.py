@@ -77,6 +77,7 @@ def main():
                                 "subnormal_ref_values": int(sub.sum()),
                                 "flushed_to_zero": int((sub & (got == 0)).sum()),
                                 "max_rel_normal": ou.max_rel_normal(got, ref),
+                                "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0)),
                                 "max_ulp": int(ou.ulp_diff(got, ref).max())}
                 for lane, e in list(zip(bad_lane, expl))[:args.max_keep]:
                     rows.append((name, si, btag, int(lane), din[:, lane], dout[:, lane], got[:, lane], ref[:, lane], e))
