@@ -228,36 +228,65 @@ struct He
     return (sigma0 > kEpsF) ? r : 0.0f;
   }
 
-  // D (he.h:411-467), Eqs. 78-79: Taylor series in g with Beckmann's rough approximation blended in
-  __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
+  // D (he.h:411-467), Eqs. 78-79: Taylor series in g with Beckmann's rough approximation blended in.  Split in two
+  // for the compaction kernel's two-phase evaluation (kernels.hpp, k_eval_pdf_compact): D_prep everything before
+  // the series (sigma's Newton steps, g, the exponent bases, the rough approximation), D_series the series itself
+  // and the blend; D = both, in order, so every path evaluates the same operations on the same operands.
+  struct DPrep { float gg[3], eb[3], rough[3]; };
+
+  __device__ __forceinline__ void D_prep(v3 in, v3 out, DPrep& d) const
   {
     const float vxy2 = sqnorm2(in.x + out.x, in.y + out.y);
     const float sg = sigma(in, out);
-    double g[3], norm[3];
-    float eb[3];
     const float tau2 = float(double(tau) * double(tau));
     const float base = (vxy2 * tau2) / 4.0f;
+    double g[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c)
     {
-      const float gg = div_nr((kPi2F * sg) * (in.z + out.z), kWavelength[c]);
-      g[c] = double(gg) * double(gg);
+      d.gg[c] = div_nr((kPi2F * sg) * (in.z + out.z), kWavelength[c]);
+      g[c] = double(d.gg[c]) * double(d.gg[c]);
       const double l2 = double(kWavelength[c]) * double(kWavelength[c]);
-      norm[c] = double(kPiSqQuarterF * tau2) * (1.0 / l2);   // constant reciprocal: within an ulp of the quotient
-      eb[c] = WESTIN ? float(double(base) * (double(kPiSqFourF) / l2)) : base;
+      d.eb[c] = WESTIN ? float(double(base) * (double(kPiSqFourF) / l2)) : base;
     }
     const double gmin = fmin(fmin(g[0], g[1]), g[2]);
-    float rough[3] = {0.0f, 0.0f, 0.0f}, weight = 0.0f;
+    d.rough[0] = d.rough[1] = d.rough[2] = 0.0f;
     if (APPROX >= 0 && gmin > double(APPROX))
     {
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
         const double rg = ddiv_nr(1.0, g[c]);    // g > APPROX here
-        rough[c] = float(exp_dd(-double(eb[c]) * rg) * rg);   // exp(-eb / g) / g in double, one rounding
+        d.rough[c] = float(exp_dd(-double(d.eb[c]) * rg) * rg);   // exp(-eb / g) / g in double, one rounding
       }
-      weight = float(fmin(fmax(gmin - double(APPROX), 0.0), 1.0));
     }
+  }
+
+  // series length key of the two-phase kernel: lanes with a similar peak position g run similar numbers of terms
+  // (0: no series -- the rough approximation alone)
+  __device__ __forceinline__ int D_key(const DPrep& d) const
+  {
+    const double g1 = double(d.gg[1]) * double(d.gg[1]);
+    const double gmin = fmin(fmin(double(d.gg[0]) * double(d.gg[0]), g1), double(d.gg[2]) * double(d.gg[2]));
+    if ((APPROX >= 0) && (gmin - 1.0 > double(APPROX))) return 0;
+    return 1 + min(30, int(float(g1) * 1.5f));
+  }
+
+  __device__ __forceinline__ void D_series(const DPrep& d, float* Dout) const
+  {
+    double g[3], norm[3];
+    float eb[3];
+    const float tau2 = float(double(tau) * double(tau));
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      g[c] = double(d.gg[c]) * double(d.gg[c]);
+      const double l2 = double(kWavelength[c]) * double(kWavelength[c]);
+      norm[c] = double(kPiSqQuarterF * tau2) * (1.0 / l2);   // constant reciprocal: within an ulp of the quotient
+      eb[c] = d.eb[c];
+    }
+    const double gmin = fmin(fmin(g[0], g[1]), g[2]);
+    const float weight = (APPROX >= 0 && gmin > double(APPROX)) ? float(fmin(fmax(gmin - double(APPROX), 0.0), 1.0)) : 0.0f;
     float sum[3] = {0.0f, 0.0f, 0.0f}, gm[3] = {1.0f, 1.0f, 1.0f}, term[3] = {0.0f, 0.0f, 0.0f}, last[3];
     bool converged = (APPROX >= 0) && (gmin - 1.0 > double(APPROX));
     // term = float(exp(-g - eb/m) gm / m) in double (he.h:454), gm = float(gm * (g / m)) rounded per step
@@ -355,51 +384,120 @@ struct He
       }
     }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], rough[c], weight)));
+    for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], d.rough[c], weight)));
   }
 
-  // he_base::eval (he.h:142-166), x albedo when scaled (scaledmodel.h:50-53); the sampler's backscatter
-  // evaluations (k_he_cdf) see the unscaled he_base, which scaledmodel wraps from outside
-  template<bool SCALE = true>
-  __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
+  __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
   {
-    const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
-    float Dv[3], F[3];
+    DPrep d;
+    D_prep(in, out, d);
+    D_series(d, Dout);
+  }
+
+
+  // he_base::eval (he.h:142-166), x albedo when scaled (scaledmodel.h:50-53); the sampler's backscatter
+  // evaluations (k_he_cdf) see the unscaled he_base, which scaledmodel wraps from outside.  Two stages, as D:
+  // eval_prep the prefactor ((1 / (pi z_i z_o)) F) S G per channel and D_prep; eval_finish the series and the
+  // product.
+  struct EvalPrep { float pre[3]; bool active; DPrep d; };
+
+  __device__ __forceinline__ void eval_prep(v3 in, v3 out, uint32_t component, EvalPrep& e) const
+  {
+    e.active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    float F[3];
     const float S = S1(in) * S1(out);
     const float Gv = G(in, out);
-    D(in, out, Dv);
+    D_prep(in, out, e.d);
     // float(safe_sqrt(double(1 + dot) / 2.0)): halving the float sum is exact in float (1 + dot >= 2^-24 or 0),
     // and the double-then-float sqrt equals the float sqrt (53 >= 2 x 24 + 2)
     const float cth = safe_sqrtf((1 + dot3(in, out)) * 0.5f);
     fres.eval3(cth, F);
     const float nrm = div_nr(1.0f, (kPiF * in.z) * out.z);
 #pragma unroll
+    for (int c = 0; c < 3; ++c) e.pre[c] = ((nrm * F[c]) * S) * Gv;
+  }
+
+  template<bool SCALE = true>
+  __device__ __forceinline__ void eval_finish(const EvalPrep& e, float* rgb) const
+  {
+    float Dv[3];
+    D_series(e.d, Dv);
+#pragma unroll
     for (int c = 0; c < 3; ++c)
     {
-      float v = (((nrm * F[c]) * S) * Gv) * Dv[c];
+      float v = e.pre[c] * Dv[c];
       if (SCALED && SCALE) v *= albedo[c];
-      rgb[c] = active ? v : 0.0f;
+      rgb[c] = e.active ? v : 0.0f;
     }
+  }
+
+  template<bool SCALE = true>
+  __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
+  {
+    EvalPrep e;
+    eval_prep(in, out, component, e);
+    eval_finish<SCALE>(e, rgb);
   }
 
   // ndf::sampler::pdf (ndf/sampler.h:102-128) of the halfway vector m
   __device__ __forceinline__ float sampler_pdf(v3 m) const { return ndf_sampler_pdf(cdf, m); }
+
+  // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156): sampler pdf of h / |4 out.h|, z(in), z(out) > 0
+  __device__ __forceinline__ float pdf_of(v3 in, v3 out, uint32_t component) const
+  {
+    const bool active = (out.z > 0) && (in.z > 0) && !masked(component);
+    const v3 h = halfway(in, out);
+    const float p = float(double(sampler_pdf(h)) / fabs(4.0 * double(dot3(out, h))));
+    return active ? p : 0.0f;
+  }
 
   template<int MODE>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     if (MODE & kModeEval) eval_rgb(in, out, component, rgb);
     else rgb[0] = rgb[1] = rgb[2] = 0.0f;
-    if (MODE & kModePdf)
-    {
-      // ndf_sampler::pdf (bbm/ndf_sampler.h:128-156): sampler pdf of h / |4 out.h|, z(in), z(out) > 0
-      const bool active = (out.z > 0) && (in.z > 0) && !masked(component);
-      const v3 h = halfway(in, out);
-      const float p = float(double(sampler_pdf(h)) / fabs(4.0 * double(dot3(out, h))));
-      pdf = active ? p : 0.0f;
-    }
-    else pdf = 0.0f;
+    pdf = (MODE & kModePdf) ? pdf_of(in, out, component) : 0.0f;
   }
+
+  // the compaction kernel's two-phase evaluation (kernels.hpp): stage 1 everything but the series, with its
+  // length key; stage 2 the series and the product -- the same operations as eval_pdf, split at the series
+#ifndef BBM_HIP_HE_ONEPHASE
+  static constexpr bool kTwoPhase = true;
+#endif
+  struct Stage { EvalPrep e; float pdf; };
+  static constexpr int kStageWords = 14;
+  __device__ __forceinline__ static void stage_store(const Stage& st, float* base, int stride)
+  {
+    for (int c = 0; c < 3; ++c)
+    {
+      base[c * stride] = st.e.pre[c];
+      base[(3 + c) * stride] = st.e.d.gg[c];
+      base[(6 + c) * stride] = st.e.d.eb[c];
+      base[(9 + c) * stride] = st.e.d.rough[c];
+    }
+    base[12 * stride] = st.e.active ? 1.0f : 0.0f;
+    base[13 * stride] = st.pdf;
+  }
+  __device__ __forceinline__ static void stage_load(Stage& st, const float* base, int stride)
+  {
+    for (int c = 0; c < 3; ++c)
+    {
+      st.e.pre[c] = base[c * stride];
+      st.e.d.gg[c] = base[(3 + c) * stride];
+      st.e.d.eb[c] = base[(6 + c) * stride];
+      st.e.d.rough[c] = base[(9 + c) * stride];
+    }
+    st.e.active = base[12 * stride] != 0.0f;
+    st.pdf = base[13 * stride];
+  }
+  template<int MODE>
+  __device__ __forceinline__ int stage1(v3 in, v3 out, uint32_t component, Stage& st) const
+  {
+    eval_prep(in, out, component, st.e);
+    st.pdf = (MODE & kModePdf) ? pdf_of(in, out, component) : 0.0f;
+    return D_key(st.e.d);
+  }
+  __device__ __forceinline__ void stage2(const Stage& st, float* rgb) const { eval_finish(st.e, rgb); }
 
   // he_base::reflectance (he.h:230-244): Fresnel at z(out) / Pi * 4.0, x albedo when scaled
   __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const

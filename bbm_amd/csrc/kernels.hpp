@@ -320,12 +320,29 @@ inline bool use_compact()
 #define BBM_HIP_COMPACT_WAVES 4
 #endif
 #define BBM_HIP_COMPACT_ATTR __attribute__((amdgpu_waves_per_eu(BBM_HIP_COMPACT_WAVES, 8)))
+// models whose evaluation splits into a prelude and a variable-length series (He): stage1 / stage2 / Stage
+constexpr int kSortBuckets = 32;
+template<class Model, int MODE> constexpr bool two_phase()
+{
+  if constexpr (requires { Model::kTwoPhase; }) return (MODE & kModeEval) != 0;
+  else return false;
+}
+template<class Model> constexpr int stage_words()
+{
+  if constexpr (requires { Model::kStageWords; }) return Model::kStageWords;
+  else return 1;
+}
+
 template<class Model, int MODE, bool MASK>
 __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compact(EvalArgs a)
 {
   constexpr int kTile = 4 * kBlock;
   __shared__ float job[6][kTile];      // live pairs' in.xyz, out.xyz; rows 0..3 then hold rgb, pdf
   __shared__ int wave_total[kBlock / 64];
+  // two-phase models only (the arrays are unused, and removed by the compiler, otherwise): 14 KiB of stage state
+  __shared__ float stage[two_phase<Model, MODE>() ? stage_words<Model>() : 1][kBlock];
+  __shared__ short origin[kBlock];
+  __shared__ int bucket[kSortBuckets], bucket_off[kSortBuckets];
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t tiles = (n4 + kBlock - 1) / kBlock;
@@ -383,14 +400,70 @@ __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compac
       }
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < total; q += kBlock)
+    if constexpr (two_phase<Model, MODE>())
     {
-      float rgb[3], pdf;
-      m.template eval_pdf<MODE>(mk3(job[0][q], job[1][q], job[2][q]), mk3(job[3][q], job[4][q], job[5][q]),
-                                a.component, rgb, pdf);
-      job[0][q] = rgb[0]; job[1][q] = rgb[1]; job[2][q] = rgb[2]; job[3][q] = pdf;
+      // Two-phase evaluation, 256 jobs at a time: stage 1 (everything but the He series) one job per thread,
+      // then the jobs are counting-sorted by the series-length key (32 buckets, LDS) and stage 2 (the series)
+      // runs in key order, so each wave takes jobs of similar length: a wave runs as many terms as its longest
+      // job, and mixing short and long series had each wave pay the longest one (wave-max / mean 1.5).  Every
+      // job is still the model's own eval on the same operands, split at the series: results are bit-identical.
+      for (int q0 = 0; q0 < total; q0 += kBlock)
+      {
+        const int q = q0 + int(threadIdx.x);
+        const bool mine = q < total;
+        typename Model::Stage st;
+        int key = 0;
+        if (mine)
+          key = m.template stage1<MODE>(mk3(job[0][q], job[1][q], job[2][q]), mk3(job[3][q], job[4][q], job[5][q]),
+                                        a.component, st);
+        if (threadIdx.x < kSortBuckets) bucket[threadIdx.x] = 0;
+        __syncthreads();
+        const int rank = mine ? atomicAdd(&bucket[key], 1) : 0;
+        __syncthreads();
+        if (threadIdx.x < 64)
+        {
+          // exclusive prefix of the bucket counts (one wave, kSortBuckets <= 64)
+          const int c = (threadIdx.x < kSortBuckets) ? bucket[threadIdx.x] : 0;
+          int incl = c;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1)
+          {
+            const int v = __shfl_up(incl, d, 64);
+            if (int(threadIdx.x) >= d) incl += v;
+          }
+          if (threadIdx.x < kSortBuckets) bucket_off[threadIdx.x] = incl - c;
+        }
+        __syncthreads();
+        if (mine)
+        {
+          const int pos = bucket_off[key] + rank;
+          Model::stage_store(st, &stage[0][pos], kBlock);
+          origin[pos] = short(q);
+        }
+        __syncthreads();
+        if (q0 + int(threadIdx.x) < total)
+        {
+          typename Model::Stage s2;
+          Model::stage_load(s2, &stage[0][threadIdx.x], kBlock);
+          float rgb[3];
+          m.stage2(s2, rgb);
+          const int o = origin[threadIdx.x];
+          job[0][o] = rgb[0]; job[1][o] = rgb[1]; job[2][o] = rgb[2]; job[3][o] = s2.pdf;
+        }
+        __syncthreads();
+      }
     }
-    __syncthreads();
+    else
+    {
+      for (int q = threadIdx.x; q < total; q += kBlock)
+      {
+        float rgb[3], pdf;
+        m.template eval_pdf<MODE>(mk3(job[0][q], job[1][q], job[2][q]), mk3(job[3][q], job[4][q], job[5][q]),
+                                  a.component, rgb, pdf);
+        job[0][q] = rgb[0]; job[1][q] = rgb[1]; job[2][q] = rgb[2]; job[3][q] = pdf;
+      }
+      __syncthreads();
+    }
     if (have)
     {
       float r[4], g[4], b[4], p[4];

@@ -70,6 +70,33 @@ __device__ __forceinline__ float div_nr(float n, float d)
   return __builtin_isnormal(q1) ? q1 : q;
 }
 
+// a / d for the quotients that are a normal float or exactly 0 on every lane whose result is used (a finite
+// nonzero divisor bounded away from the subnormal range, e.g. 1 / |h| with |h|^2 in (0, 4], or Fresnel's
+// (g - c) / (g + c) with c > 0): the Markstein step alone, no special-case select.  Same result as div_nr there.
+__device__ __forceinline__ float div_nr_n(float n, float d)
+{
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float q = n * r;
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+}
+
+// sqrtf (IEEE, correctly rounded) as v_rsq_f32 and one Newton/Markstein step: s = x rsq(x), h = rsq(x) / 2,
+// s' = s + (x - s^2) h with the residual x - s^2 exact (FMA) -- the correctly rounded root except within ~2^-22 ulp
+// of a rounding midpoint (a root is never exactly one), ~7 VALU against the compiler's ~14-instruction sequence
+// with its denormal scaling.  Zero, subnormal, infinite and NaN arguments take the hardware root (0, inf and NaN
+// exact; a subnormal argument to ~1 ulp).
+__device__ __forceinline__ float sqrt_nr(float x)
+{
+#ifdef BBM_HIP_SQRT_IEEE
+  return sqrtf(x);
+#else
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s = x * y;
+  const float s1 = __builtin_fmaf(__builtin_fmaf(-s, s, x), 0.5f * y, s);
+  return __builtin_isnormal(x) ? s1 : __builtin_amdgcn_sqrtf(x);
+#endif
+}
+
 // ---------------------------------------------------------------- exponentials and powers
 //
 // Measured on gfx950 (tools/hwmath_probe.hip, every float in range): v_log_f32 is within 2.0 * 2^-24 relative of
@@ -173,7 +200,12 @@ __device__ __forceinline__ float expf_glibc(float x)
   const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
   const double kd = kb - kShift;
   const double r = __builtin_fma(kInvLn2N, xd, -kd);             // x N / ln2 - k, |r| <= 1/2
+#ifdef BBM_HIP_EXPF_NOGATHER_TIMING
+  // timing probe only (tools/build_variant.sh): the table gather replaced by arithmetic of the same shape (wrong values)
+  const double s = __builtin_bit_cast(double, (0x3fef000000000000ull | ((ki & 31u) << 40)) + (ki << 47));
+#else
   const double s = __builtin_bit_cast(double, kExpfTab[ki & 31u] + (ki << 47));   // 2^(k/N)
+#endif
   const double z = __builtin_fma(kC0, r, kC1);
   const double r2 = r * r;
   double y = __builtin_fma(kC2, r, 1.0);
@@ -181,6 +213,26 @@ __device__ __forceinline__ float expf_glibc(float x)
   const float res = float(y * s);
   // |x| >= 88 or NaN in glibc: -inf and x < log(2^-150) -> 0, x > log(2^128) -> inf, NaN -> NaN (via res)
   return (x < -0x1.9fe368p6f) ? 0.0f : ((x > 0x1.62e42ep6f) ? __builtin_inff() : res);
+}
+// the same for x <= 0 or NaN (an exponent that is minus a square or a quotient of squares): no overflow select
+__device__ __forceinline__ float expf_glibc_neg(float x)
+{
+  constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
+  constexpr double kShift = 0x1.8p+52;
+  constexpr double kC0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, kC1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+                   kC2 = 0x1.62e42ff0c52d6p-1 / 32;
+  const double xd = double(x);
+  const double kb = __builtin_fma(kInvLn2N, xd, kShift);
+  const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
+  const double kd = kb - kShift;
+  const double r = __builtin_fma(kInvLn2N, xd, -kd);
+  const double s = __builtin_bit_cast(double, kExpfTab[ki & 31u] + (ki << 47));
+  const double z = __builtin_fma(kC0, r, kC1);
+  const double r2 = r * r;
+  double y = __builtin_fma(kC2, r, 1.0);
+  y = __builtin_fma(z, r2, y);
+  const float res = float(y * s);
+  return (x < -0x1.9fe368p6f) ? 0.0f : res;
 }
 
 // a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
@@ -327,7 +379,7 @@ __device__ __forceinline__ float sqnorm2(float a, float b) { return (0.0f + a * 
 // horizontal.h:96-100 normalize = t * rsqrt(|t|^2); math.h:109-112 rsqrt = rcp(sqrt) = 1 / sqrt
 __device__ __forceinline__ v3 normalize3(v3 t)
 {
-  const float r = div_nr(1.0f, sqrtf(dot3(t, t)));
+  const float r = div_nr_n(1.0f, sqrt_nr(dot3(t, t)));   // |t|^2 of a sum of two unit vectors: 1 / |t| normal
   return mk3(t.x * r, t.y * r, t.z * r);
 }
 
@@ -341,13 +393,13 @@ __device__ __forceinline__ v3 cross3(v3 a, v3 b)
 }
 
 // math.h:129 safe_sqrt = sqrt(std::max(a, T(0))): std::max keeps a NaN argument (a < 0 is false)
-__device__ __forceinline__ float safe_sqrtf(float a) { return sqrtf((a < 0.0f) ? 0.0f : a); }
+__device__ __forceinline__ float safe_sqrtf(float a) { return sqrt_nr((a < 0.0f) ? 0.0f : a); }
 __device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
 
 // core/spherical.h:79-80 sinTheta2 = bbm::max(1 - z*z, 0) -> fmaxf (result_t<float,int> = float)
 __device__ __forceinline__ float sin_theta2(v3 v) { return fmaxf(1 - v.z * v.z, 0.0f); }
 // spherical.h:179-180 tanTheta = sinTheta / cosTheta; :185-186 tanTheta2 = sinTheta2 / cosTheta2
-__device__ __forceinline__ float tan_theta(v3 v) { return div_nr(sqrtf(sin_theta2(v)), v.z); }
+__device__ __forceinline__ float tan_theta(v3 v) { return div_nr(sqrt_nr(sin_theta2(v)), v.z); }
 __device__ __forceinline__ float tan_theta2(v3 v) { return div_nr(sin_theta2(v), v.z * v.z); }
 
 // std::clamp(a, T(lo), T(hi)) (backbone/native/include/backbone/math.h:106-107)
@@ -373,6 +425,7 @@ __device__ __forceinline__ void cossin_phi(v3 v, float& c, float& s)
 // w = float(-log((1 - a)(1 + a))): the reference's log is f64; here -log1p(-a^2) in f32 (a^2 as an exact
 // two-product, log1p by the u = 1 + x correction on the device logf, ~2 ulp) -- ~20 VALU instead of ~100 f64
 // instructions; the five erfinv calls of a Beckmann sample were its whole cost.
+#ifdef BBM_HIP_ERFINV_V1
 __device__ __forceinline__ float erfinv_w(float a)
 {
   const float a2 = a * a;
@@ -381,11 +434,28 @@ __device__ __forceinline__ float erfinv_w(float a)
   const float l1p = (u == 1.0f) ? -a2 : logf(u) * div_nr(-a2, u - 1.0f);
   return (u == 0.0f) ? __builtin_inff() : -(l1p - div_nr(a2e, u));   // a = +-1: -log(0) = inf
 }
+#else
+// The same w on the transcendental unit: u = 1 - a^2 is a normal float in [2^-24, 1] (or 0, or 1), so v_log_f32
+// (2 2^-24 relative in log2 u, x -> 1 included) times ln 2 replaces the library logf, and the two correction
+// factors -a2 / (u - 1) (= 1 + O(2^-24)) and a2e / u (a rounding residue) need no Newton step: w moves by <= 2 ulp
+// against the library form, inside the ~2-ulp spread the f32 w already has against the reference's double w.
+__device__ __forceinline__ float erfinv_w(float a)
+{
+  const float a2 = a * a;
+  const float a2e = __builtin_fmaf(a, a, -a2);          // a^2 = a2 + a2e exactly
+  const float u = 1.0f - a2;
+  const float lu = (__builtin_amdgcn_logf(u) * kLn2F) * (-a2 * __builtin_amdgcn_rcpf(u - 1.0f));
+  const float l1p = (u == 1.0f) ? -a2 : lu;
+  return (u == 0.0f) ? __builtin_inff() : -(l1p - a2e * __builtin_amdgcn_rcpf(u));   // a = +-1: -log(0) = inf
+}
+#endif
 __device__ __forceinline__ float erfinv_f(float a)
 {
   const float w = erfinv_w(a);
   float p;
+#ifdef BBM_HIP_ERFINV_V1
   if (w < 5)
+#endif
   {
     const float x = w - 2.5f;
     p = 2.81022636e-08f;
@@ -394,14 +464,25 @@ __device__ __forceinline__ float erfinv_f(float a)
     p = __builtin_fmaf(p, x, -0.00125372503f); p = __builtin_fmaf(p, x, -0.00417768164f);
     p = __builtin_fmaf(p, x, 0.246640727f); p = __builtin_fmaf(p, x, 1.50140941f);
   }
+#ifdef BBM_HIP_ERFINV_V1
   else
+#else
+  // the tail (w >= 5: |a| > 0.9966) only where some lane of the wave needs it (a wave-uniform branch; the sampler
+  // reaches it at grazing stretched views and for xi near 0 or 1): the central polynomial is not evaluated twice
+  if (__builtin_amdgcn_ballot_w64(!(w < 5)) != 0)
+#endif
   {
     const float x = sqrtf(w) - 3.0f;
-    p = -0.000200214257f;
-    p = __builtin_fmaf(p, x, 0.000100950558f); p = __builtin_fmaf(p, x, 0.00134934322f);
-    p = __builtin_fmaf(p, x, -0.00367342844f); p = __builtin_fmaf(p, x, 0.00573950773f);
-    p = __builtin_fmaf(p, x, -0.0076224613f); p = __builtin_fmaf(p, x, 0.00943887047f);
-    p = __builtin_fmaf(p, x, 1.00167406f); p = __builtin_fmaf(p, x, 2.83297682f);
+    float q = -0.000200214257f;
+    q = __builtin_fmaf(q, x, 0.000100950558f); q = __builtin_fmaf(q, x, 0.00134934322f);
+    q = __builtin_fmaf(q, x, -0.00367342844f); q = __builtin_fmaf(q, x, 0.00573950773f);
+    q = __builtin_fmaf(q, x, -0.0076224613f); q = __builtin_fmaf(q, x, 0.00943887047f);
+    q = __builtin_fmaf(q, x, 1.00167406f); q = __builtin_fmaf(q, x, 2.83297682f);
+#ifdef BBM_HIP_ERFINV_V1
+    p = q;
+#else
+    p = (w < 5) ? p : q;
+#endif
   }
   return p * a;
 }

@@ -43,7 +43,7 @@ struct Beckmann
 #elif defined(BBM_HIP_BECKMANN_EXP_RN)
     float D = div_nr(expf_rn(div_nr(-sn, c2)), au * av * c2 * c2);      // A/B: correctly rounded
 #else
-    float D = div_nr(expf_glibc(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit
+    float D = div_nr(expf_glibc_neg(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit (x <= 0)
 #endif
     if (Normalize) D *= kInvPiF;
     return (h.z > 0) ? D : 0.0f;
@@ -397,8 +397,10 @@ struct FresnelCook
   __device__ __forceinline__ float eval(float c) const
   {
     const float g = safe_sqrtf(eta * eta + c * c - 1.0f);
-    const float a = div_nr(g - c, g + c);
-    const float b = div_nr(c * (g + c) - 1.0f, c * (g - c) + 1.0f);
+    // c = (in.h + out.h) / 2 > 0 where the result is used, g >= 0, and for eta >= 1 (its lower bound) g - c =
+    // (eta^2 - 1) / (g + c) >= 0: both denominators are normal and positive, both quotients normal or 0
+    const float a = div_nr_n(g - c, g + c);
+    const float b = div_nr_n(c * (g + c) - 1.0f, c * (g - c) + 1.0f);
     return fmaxf(0.5f * (a * a) * (1.0f + b * b), 0.0f);   // bbm::max(x, 0.0): fmax in double == fmaxf here
   }
 };

@@ -38,6 +38,9 @@ template<> struct eval_waves<Bagher> { static constexpr int value = BBM_HIP_BAGH
 
 // Compositions (reference file:line):
 using CookTorranceM = Microfacet<Beckmann<false, false>, VGroove, FresnelCook, Norm::Cook, true>;         // bsdfmodel/cooktorrance.h:28-34
+#ifdef BBM_HIP_CT_WAVES
+template<> struct eval_waves<CookTorranceM> { static constexpr int value = BBM_HIP_CT_WAVES; };   // A/B
+#endif
 using GGXM = Microfacet<GGX<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                        // bsdfmodel/ggx.h:27-33
 using CookTorranceWalterM = Microfacet<Beckmann<false, true>, Uncorrelated, FresnelCook, Norm::Walter, true>;  // bsdfmodel/cooktorrancewalter.h:32-38
 
