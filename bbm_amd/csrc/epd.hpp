@@ -162,7 +162,7 @@ struct EpdNdf
   {
     const float c2 = h.z * h.z;
     const float t2 = div_nr(1 - c2, c2);
-    const float D = div_nr(normalization * expf_dn(-powf_acc(div_nr(t2, beta * beta), p)), c2 * c2);
+    const float D = div_nr(normalization * expf_lobe(-powf_acc(div_nr(t2, beta * beta), p)), c2 * c2);
     return (h.z > 0) ? D : 0.0f;
   }
 

@@ -38,6 +38,125 @@ __device__ __forceinline__ double tan_theta(d3 v) { return sqrt(sin_theta2(v)) /
 __device__ __forceinline__ double tan_theta2(d3 v) { return sin_theta2(v) / (v.z * v.z); }   // spherical.h:186
 __device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
 
+// ---------------------------------------------------------------- exp / log / pow in double
+//
+// The reference's doubleRGB exp / log / pow are glibc's (correctly rounded, or within ~0.52 ulp).  ocml's f64 pow
+// carries its logarithm in double-double and is the bulk of the pow-heavy models' VALU per pair; these
+// restatements stay within a few ulp of glibc at about half the cost (tools/f64math_probe.hip measures them
+// against the host libm), far inside the doubleRGB bar (1e-10 relative, tests/test_gpu_f64.py).
+//
+// 2^f - 1 for |f| <= 1/2: f (c1 + f (c2 + ... c13)), the degree-13 Taylor polynomial of e^(f ln2) - 1
+// (truncation <= 1e-17 relative); no 1 is added, so 2^f - 1 keeps its relative precision as f -> 0
+__device__ __forceinline__ double exp2m1_poly(double f)
+{
+  double p = 0x1.816193166d0f9p-40;
+  p = __builtin_fma(p, f, 0x1.c3bd650fc2986p-36);
+  p = __builtin_fma(p, f, 0x1.e8cac7351bb25p-32);
+  p = __builtin_fma(p, f, 0x1.e4cf5158b8ecap-28);
+  p = __builtin_fma(p, f, 0x1.b5253d395e7c4p-24);
+  p = __builtin_fma(p, f, 0x1.62c0223a5c824p-20);
+  p = __builtin_fma(p, f, 0x1.ffcbfc588b0c7p-17);
+  p = __builtin_fma(p, f, 0x1.430912f86c787p-13);
+  p = __builtin_fma(p, f, 0x1.5d87fe78a6731p-10);
+  p = __builtin_fma(p, f, 0x1.3b2ab6fba4e77p-7);
+  p = __builtin_fma(p, f, 0x1.c6b08d704a0c0p-5);
+  p = __builtin_fma(p, f, 0x1.ebfbdff82c58fp-3);
+  p = __builtin_fma(p, f, 0x1.62e42fefa39efp-1);
+  return p * f;
+}
+
+// 2^t over the whole double range: n = rint(t), 2^(t - n) (t - n exact) scaled by 2^n in one rounding, subnormal
+// results included; overflow to inf, 0 far below 2^-1074, NaN propagates
+__device__ __forceinline__ double exp2_d(double t)
+{
+  const double n = __builtin_rint(t);
+  const double r = __builtin_ldexp(1.0 + exp2m1_poly(t - n), int(__builtin_fmin(__builtin_fmax(n, -1100.0), 1100.0)));
+  return (t < -1100.0) ? 0.0 : ((t > 1100.0) ? __builtin_inf() : r);
+}
+
+// e^a: n = rint(a / ln2), r = a - n ln2 in two FMAs (Cody-Waite; n ln2_hi exact), e^r - 1 by its degree-13
+// Taylor polynomial on |r| <= 0.35 (truncation 1e-17): ~1 ulp over the whole range, subnormal results included
+__device__ __forceinline__ double exp_d(double a)
+{
+#ifdef BBM_HIP_F64_OCML
+  return exp(a);   // A/B: the device library (tools/build_variant.sh)
+#endif
+  const double n = __builtin_rint(a * 0x1.71547652b82fep0);
+  double r = __builtin_fma(-n, 0x1.62e42fefa3800p-1, a);
+  r = __builtin_fma(-n, 0x1.ef35793c76730p-45, r);
+  double p = 1.0 / 6227020800.0;                         // 1 / 13!
+  p = __builtin_fma(p, r, 1.0 / 479001600.0);
+  p = __builtin_fma(p, r, 1.0 / 39916800.0);
+  p = __builtin_fma(p, r, 1.0 / 3628800.0);
+  p = __builtin_fma(p, r, 1.0 / 362880.0);
+  p = __builtin_fma(p, r, 1.0 / 40320.0);
+  p = __builtin_fma(p, r, 1.0 / 5040.0);
+  p = __builtin_fma(p, r, 1.0 / 720.0);
+  p = __builtin_fma(p, r, 1.0 / 120.0);
+  p = __builtin_fma(p, r, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  const double v = __builtin_ldexp(__builtin_fma(p, r, 1.0), int(__builtin_fmin(__builtin_fmax(n, -1100.0), 1100.0)));
+  return (a < -746.0) ? 0.0 : ((a > 710.0) ? __builtin_inf() : v);
+}
+
+// log2(x) for finite x > 0 (subnormals included) to ~1 ulp + 2^-53 absolute: x = 2^k m with m in [1/sqrt2, sqrt2),
+// l0 = v_log_f32(m) (|l0| <= 1/2, 2^-23 relative), one Newton step on 2^L = m: e = m 2^-l0 - 1
+// = (m - 1)(1 + q) + q with q = 2^-l0 - 1 (|e| < 2^-21; m - 1 exact), L = l0 + log2(1 + e) by three terms.
+// Near x = 1 (k = 0) the result keeps its relative precision.
+__device__ __forceinline__ double log2_d(double x)
+{
+  double m = __builtin_amdgcn_frexp_mant(x);             // [1/2, 1)
+  int k = __builtin_amdgcn_frexp_exp(x);
+  const bool lo = m < 0.70710678118654752;
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const float l0 = __builtin_amdgcn_logf(float(m));
+  const double q = exp2m1_poly(-double(l0));
+  const double e = __builtin_fma(m - 1.0, 1.0 + q, q);
+  const double l1p = e * __builtin_fma(e, __builtin_fma(e, 1.0 / 3.0, -0.5), 1.0);
+  return double(k) + __builtin_fma(l1p, 0x1.71547652b82fep0, double(l0));
+}
+
+// glibc's log restated on log2_d (x < 0 -> NaN; x = 0 -> -inf; inf -> inf; NaN -> NaN)
+__device__ __forceinline__ double log_d(double x)
+{
+#ifdef BBM_HIP_F64_OCML
+  return log(x);
+#endif
+  const double v = log2_d(x) * 0x1.62e42fefa39efp-1;
+  return (x == 0.0) ? -__builtin_inf() : ((x < 0.0) ? __builtin_nan("") : ((x == __builtin_inf()) ? x : v));
+}
+// x^y for x >= 0 (or NaN) and finite y: 2^(y log2 x), y log2 x to ~2^-52 relative + |y| 2^-53 absolute (~1e-13
+// relative on every result above the subnormal range); pow(x, 0) = pow(1, y) = 1, pow(0, y) = 0 / inf,
+// pow(inf, y) = inf / 0, x < 0 -> NaN (never reached: the reference's bases here are >= 0)
+__device__ __forceinline__ double pow_d(double x, double y)
+{
+#ifdef BBM_HIP_F64_OCML
+  return pow(x, y);
+#endif
+  double r = exp2_d(y * log2_d(x));
+  const bool big = x == __builtin_inf();
+  r = (x == 0.0 || big) ? (((y > 0.0) == big) ? __builtin_inf() : 0.0) : r;
+  r = (x < 0.0) ? __builtin_nan("") : r;
+  return (y == 0.0 || x == 1.0) ? 1.0 : r;
+}
+// x^5 for the Schlick / Bagher / Ashikhmin-Shirley factors (1 - c)^5, as glibc's pow(x, 5.0) rounds it: the
+// power carried as a double-double through three exact products (two FMA residuals each), rounded once -- the
+// correctly rounded x^5 but within ~2^-45 ulp of a midpoint.  These factors feed the reflectance weights that
+// pick an aggregate's child at xi0 = 1, where an ulp of a weight decides the pick (tests/test_gpu_f64.py).
+__device__ __forceinline__ double pow5_d(double x)
+{
+#ifdef BBM_HIP_F64_OCML
+  return pow(x, 5.0);
+#endif
+  const double x2 = x * x, e2 = __builtin_fma(x, x, -x2);                                   // x^2 = x2 + e2
+  const double x4 = x2 * x2, e4 = __builtin_fma(x2, x2, -x4) + 2.0 * x2 * e2;              // x^4 ~ x4 + e4
+  const double x5 = x4 * x, e5 = __builtin_fma(x4, x, -x5) + e4 * x;
+  return x5 + e5;
+}
+
 __device__ __forceinline__ d3 cross(d3 a, d3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 __device__ __forceinline__ bool xi_ok(double xi0, double xi1) { return (xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1); }
 // spherical.h:156-161 cossinPhi: (1, 0) at the pole, else clamp(xy / sinTheta, -1, 1)
@@ -52,7 +171,7 @@ __device__ __forceinline__ void cossin_phi(d3 v, double& c, double& s)
 // the native backbone's erfinv (backbone/native/include/backbone/math.h:115-120, Giles' polynomials) in double
 __device__ __forceinline__ double erfinv(double a)
 {
-  const double w = -log((1.0 - a) * (1.0 + a));
+  const double w = -log_d((1.0 - a) * (1.0 + a));
   double p;
   if (w < 5)
   {
@@ -89,7 +208,7 @@ struct Beckmann
   __device__ __forceinline__ double eval(d3 h) const
   {
     const double c2 = h.z * h.z;
-    double D = exp(-sqnorm2(h.x / au, h.y / av) / c2) / (au * av * c2 * c2);
+    double D = exp_d(-sqnorm2(h.x / au, h.y / av) / c2) / (au * av * c2 * c2);
     if (Normalize) D *= kInvPi;
     return (h.z > 0) ? D : 0.0;
   }
@@ -108,12 +227,12 @@ struct Beckmann
     const double maxval = erf(1.0 / tanT);
     double xc0 = fmin(fmax(xi0, 10e-6), 1.0 - 10e-6);
     const double xc1 = fmin(fmax(xi1, 10e-6), 1.0 - 10e-6);
-    double x = maxval - (maxval + 1) * erf(sqrt(-log(xc0)));
-    xc0 *= 1.0 + maxval + kInvSqrtPi * tanT * exp(-(vs.z * vs.z));
+    double x = maxval - (maxval + 1) * erf(sqrt(-log_d(xc0)));
+    xc0 *= 1.0 + maxval + kInvSqrtPi * tanT * exp_d(-(vs.z * vs.z));
     for (int i = 0; i < 3; ++i)
     {
       const double slope = erfinv(x);
-      const double val = 1.0 + x + kInvSqrtPi * tanT * exp(-slope * slope) - xc0;
+      const double val = 1.0 + x + kInvSqrtPi * tanT * exp_d(-slope * slope) - xc0;
       const double der = 1.0 - slope * tanT;
       x -= val / der;
     }
@@ -173,7 +292,7 @@ struct PhongNdf
   __device__ explicit PhongNdf(const double* p) : sharpness(p[0]) {}
   __device__ __forceinline__ double eval(d3 h) const
   {
-    const double D = pow(h.z, sharpness) * ((sharpness + 2) / (2.0 * kPi));
+    const double D = pow_d(h.z, sharpness) * ((sharpness + 2) / (2.0 * kPi));
     return (h.z > 0) ? D : 0.0;
   }
   __device__ __forceinline__ double G1(d3 v, d3 m) const
@@ -186,7 +305,7 @@ struct PhongNdf
   __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
   {
     if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
-    const double cosT = pow(xi0, 1.0 / (sharpness + 2));
+    const double cosT = pow_d(xi0, 1.0 / (sharpness + 2));
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     double sp, cp;
     sincos(xi1 * (2.0 * kPi), &sp, &cp);
@@ -204,7 +323,7 @@ struct StudentT
   {
     // parameter-only factors of G1 (studentt.h:152-156), once per thread
     lam_scale = tgamma(gamma - 0.5) / tgamma(gamma) * kInvSqrtPi;
-    s1_scale = pow(gamma - 1, gamma) / (2 * gamma - 3);
+    s1_scale = pow_d(gamma - 1, gamma) / (2 * gamma - 3);
     sqrt_g1 = sqrt(gamma - 1);
     f22 = F22(gamma);
     f23 = F23(gamma);
@@ -212,7 +331,7 @@ struct StudentT
   __device__ __forceinline__ double eval(d3 h) const
   {
     const double z2 = h.z * h.z;
-    const double den = pow(1.0 + sqnorm2(h.x / au, h.y / av) / ((gamma - 1) * z2), gamma);
+    const double den = pow_d(1.0 + sqnorm2(h.x / au, h.y / av) / ((gamma - 1) * z2), gamma);
     const double D = 1.0 / (kPi * (au * av) * (z2 * z2) * den);
     return (h.z > 0) ? D : 0.0;
   }
@@ -242,7 +361,7 @@ struct StudentT
     const bool mask = (v.z > 0) && (dot(v, m) > 0);
     const bool normal_mask = v.z < 1.0 - kEps;
     const double z = v.z * (1.0 / sqrt(sqnorm2(v.x * au, v.y * av)));
-    const double S1 = pow((gamma - 1) + z * z, 1.5 - gamma) / z;
+    const double S1 = pow_d((gamma - 1) + z * z, 1.5 - gamma) / z;
     const double S2 = F21(z) * (f22 + f23 * F24(z));
     const double lambda = normal_mask ? lam_scale * (s1_scale * S1 + sqrt_g1 * S2) - 0.5 : 0.0;
     return mask ? (normal_mask ? 1.0 / (1.0 + lambda) : 1.0) : 0.0;
@@ -266,7 +385,7 @@ struct StudentT
       cp = x * r; sp = y * r;
     }
     else normalization = au * au;
-    const double tan2 = (pow(xi1, 1.0 / (1.0 - gamma)) - 1) * (gamma - 1) * normalization;
+    const double tan2 = (pow_d(xi1, 1.0 / (1.0 - gamma)) - 1) * (gamma - 1) * normalization;
     const double cosT = 1.0 / sqrt(1.0 + tan2);
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     return mk(cp * sinT, sp * sinT, cosT);
@@ -280,21 +399,21 @@ struct LowNdf
   double B, C, norm_pdf;
   __device__ explicit LowNdf(const double* p) : B(p[0]), C(p[1])
   {
-    const double normalization = (fabs(C - 1) < kEps) ? 1.0 / log(1.0 + B) : (C - 1.0) / (1.0 - pow(1.0 + B, 1.0 - C));
+    const double normalization = (fabs(C - 1) < kEps) ? 1.0 / log_d(1.0 + B) : (C - 1.0) / (1.0 - pow_d(1.0 + B, 1.0 - C));
     norm_pdf = 0.5 * kInvPi * normalization;
   }
   // low.h:67-89: inverse of the marginal CDF of cos(theta)
   __device__ __forceinline__ d3 sample(d3, double xi0, double xi1) const
   {
     if (!xi_ok(xi0, xi1)) return mk(0.0, 0.0, 0.0);
-    const double term = (fabs(C - 1) < kEps) ? exp(xi0 * log(1.0 + B)) : pow(1.0 + xi0 * (pow(1.0 + B, 1.0 - C) - 1.0), -1.0 / (C - 1.0));
+    const double term = (fabs(C - 1) < kEps) ? exp_d(xi0 * log_d(1.0 + B)) : pow_d(1.0 + xi0 * (pow_d(1.0 + B, 1.0 - C) - 1.0), -1.0 / (C - 1.0));
     const double cosT = (1.0 + B - term) / B;
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     double sp, cp;
     sincos(xi1 * (2.0 * kPi), &sp, &cp);
     return mk(cp * sinT, sp * sinT, cosT);
   }
-  __device__ __forceinline__ double eval(d3 h) const { return (h.z > 0) ? pow(1.0 + B * (1.0 - h.z), -C) : 0.0; }
+  __device__ __forceinline__ double eval(d3 h) const { return (h.z > 0) ? pow_d(1.0 + B * (1.0 - h.z), -C) : 0.0; }
   __device__ __forceinline__ double G1(d3, d3) const { return 1.0; }
   // low.h:96-112
   __device__ __forceinline__ double pdf(d3, d3, double D) const
@@ -377,7 +496,7 @@ struct FresnelSchlick
   static constexpr int kParams = 1;
   double r0;
   __device__ explicit FresnelSchlick(const double* p) : r0(p[0]) {}
-  __device__ __forceinline__ double eval(double c) const { return r0 + (1.0 - r0) * pow(1.0 - c, 5.0); }
+  __device__ __forceinline__ double eval(double c) const { return r0 + (1.0 - r0) * pow5_d(1.0 - c); }
 };
 
 // ----------------------------------------------------------------------------------------------- models
@@ -631,13 +750,13 @@ struct Ward
     if (KIND == 0) nf = 4.0 * kPi * sqrt(in.z * out.z) * rx * ry;
     else if (KIND == 1) nf = 4.0 * kPi * rx * ry * (in.z * out.z);
     else nf = 4.0 * kPi * rx * ry * (zH2 * zH2) / dot(H, H);
-    const double f = exp(-exponent) / nf;
+    const double f = exp_d(-exponent) / nf;
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = active ? albedo[c] * f : 0.0;
     // ward.h:126-140
     const d3 h = normalize(H);
     const double np = 4.0 * kPi * rx * ry * dot(in, h) * (h.z * h.z * h.z);
-    pdf = active ? exp(-(sqnorm2(h.x / rx, h.y / ry) / (h.z * h.z))) / np : 0.0;
+    pdf = active ? exp_d(-(sqnorm2(h.x / rx, h.y / ry) / (h.z * h.z))) / np : 0.0;
   }
   __device__ __forceinline__ void reflectance(d3, uint32_t component, double* rgb) const
   {
@@ -654,7 +773,7 @@ struct Ward
     sincos(2.0 * kPi * xi0, &s, &c);
     const double cx = c * rx, cy = s * ry, r = 1.0 / sqrt(sqnorm2(cx, cy));
     const double csx = cx * r, csy = cy * r;
-    const double cosT = 1.0 / sqrt(1.0 - (log(xi1) / sqnorm2(csx / rx, csy / ry)));
+    const double cosT = 1.0 / sqrt(1.0 - (log_d(xi1) / sqnorm2(csx / rx, csy / ry)));
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     dir = reflect(out, mk(csx * sinT, csy * sinT, cosT));
     double rgb[3];
@@ -673,7 +792,7 @@ struct PhongLobe
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
-    const double pw = pow(fmax(dot(mk(-in.x, -in.y, in.z), out), 0.0), s);
+    const double pw = pow_d(fmax(dot(mk(-in.x, -in.y, in.z), out), 0.0), s);
     const double f = (s + 2) * (0.5 * kInvPi) * pw;
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = active ? albedo[c] * f : 0.0;
@@ -691,7 +810,7 @@ struct PhongLobe
     BBM_F64_SAMPLE_PROLOGUE
     double sp, cp;
     sincos(xi0 * (2.0 * kPi), &sp, &cp);
-    const double cosT = pow(xi1, 1.0 / (s + 1));
+    const double cosT = pow_d(xi1, 1.0 / (s + 1));
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     dir = to_global(mk(-out.x, -out.y, out.z), mk(cp * sinT, sp * sinT, cosT));
     double rgb[3];
@@ -710,23 +829,23 @@ struct Lafortune
   __device__ explicit Lafortune(const double* p) : cx(p[3]), cy(Aniso ? p[4] : p[3]), cz(p[Aniso ? 5 : 4]), s(p[Aniso ? 6 : 5])
   {
     albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2];
-    ngan = NGAN ? (s + 2.0) * (0.5 * kInvPi) / pow(fmax(cz * cz, cx * cx), s * 0.5) : 1.0;
+    ngan = NGAN ? (s + 2.0) * (0.5 * kInvPi) / pow_d(fmax(cz * cz, cx * cx), s * 0.5) : 1.0;
   }
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
     const bool ev = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
-    const double fr = pow(fmax(dot(mk(cx, cy, cz), mk(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0), s);
+    const double fr = pow_d(fmax(dot(mk(cx, cy, cz), mk(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0), s);
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = ev ? (NGAN ? albedo[c] * fr * ngan : albedo[c] * fr) : 0.0;
     const bool pd = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
     const d3 co = normalize(mk(cx * out.x, cy * out.y, cz * out.z));
-    pdf = pd ? (s + 1) / (2.0 * kPi) * pow(fmax(dot(co, in), 0.0), s) : 0.0;
+    pdf = pd ? (s + 1) / (2.0 * kPi) * pow_d(fmax(dot(co, in), 0.0), s) : 0.0;
   }
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
     const bool m = component & kFlagSpecular;
     const d3 co = mk(cx * out.x, cy * out.y, cz * out.z);
-    const double normalization = pow(sqrt(dot(co, co)), s) * (2.0 * kPi) / (s + 2);
+    const double normalization = pow_d(sqrt(dot(co, co)), s) * (2.0 * kPi) / (s + 2);
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = m ? (NGAN ? albedo[c] * normalization * ngan : albedo[c] * normalization) : 0.0;
   }
@@ -736,7 +855,7 @@ struct Lafortune
     BBM_F64_SAMPLE_PROLOGUE
     double sp, cp;
     sincos(xi0 * (2.0 * kPi), &sp, &cp);
-    const double cosT = pow(xi1, 1.0 / (s + 1));
+    const double cosT = pow_d(xi1, 1.0 / (s + 1));
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     dir = to_global(mk(cx * out.x, cy * out.y, cz * out.z), mk(cp * sinT, sp * sinT, cosT));
     double rgb[3];
@@ -754,7 +873,7 @@ struct FresnelSchlickRGB
   __device__ explicit FresnelSchlickRGB(const double* p) { r0[0] = p[0]; r0[1] = p[1]; r0[2] = p[2]; }
   __device__ __forceinline__ void eval3(double c, double* F) const
   {
-    const double x5 = pow(1.0 - c, 5.0);
+    const double x5 = pow5_d(1.0 - c);
 #pragma unroll
     for (int k = 0; k < 3; ++k) F[k] = r0[k] + (1.0 - r0[k]) * x5;
   }
@@ -794,7 +913,7 @@ struct AshikhminShirley
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
     const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
     const double normalization = Aniso ? sqrt((su + 1) * (sv + 1)) / (2.0 * kPi) : (su + 1.0) / (2.0 * kPi);
-    return active ? normalization * pow(h.z, exponent(h)) / (4.0 * dot(h, in)) : 0.0;
+    return active ? normalization * pow_d(h.z, exponent(h)) / (4.0 * dot(h, in)) : 0.0;
   }
   __device__ __forceinline__ double diff_albedo() const
   {
@@ -809,11 +928,11 @@ struct AshikhminShirley
     double F[3];
     fres.eval3(hdi, F);
     const double normalization = Aniso ? sqrt((su + 1) * (sv + 1)) / (8.0 * kPi) : (su + 1) / (8.0 * kPi);
-    const double np = normalization * pow(h.z, exponent(h));
+    const double np = normalization * pow_d(h.z, exponent(h));
     const double denom = hdi * fmax(in.z, out.z);
     double diff_scale = 0.0;
     if constexpr (FULL)
-      diff_scale = 28.0 / (23.0 * kPi) * ((1.0 * (1.0 - pow(1.0 - 0.5 * in.z, 5.0))) * (1.0 - pow(1.0 - 0.5 * out.z, 5.0)));
+      diff_scale = 28.0 / (23.0 * kPi) * ((1.0 * (1.0 - pow5_d(1.0 - 0.5 * in.z))) * (1.0 - pow5_d(1.0 - 0.5 * out.z)));
     const bool diff = FULL && (component & kFlagDiffuse) && upper;
 #pragma unroll
     for (int c = 0; c < 3; ++c)
@@ -862,12 +981,12 @@ struct AshikhminShirley
       double phi = atan(sqrt((su + 1.0) / (sv + 1.0)) * tan(xi0 * (2.0 * kPi)));
       phi = ((xi0 > 0.25) && (xi0 < 0.75)) ? phi + kPi : phi;
       sincos(phi, &sp, &cp);
-      cosT = pow(xi1, 1.0 / ((su * (cp * cp)) + (sv * (sp * sp)) + 1.0));
+      cosT = pow_d(xi1, 1.0 / ((su * (cp * cp)) + (sv * (sp * sp)) + 1.0));
     }
     else
     {
       sincos(xi0 * (2.0 * kPi), &sp, &cp);
-      cosT = pow(xi1, 1.0 / (su + 1.0));
+      cosT = pow_d(xi1, 1.0 / (su + 1.0));
     }
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     dir = reflect(out, mk(cp * sinT, sp * sinT, cosT));
@@ -911,7 +1030,7 @@ struct LowSmooth
     const double ro2 = sin_theta2(out);
     const double bb = B * (1.0 - ro2);
     const double t = 1.0 + (2 * B * (1.0 + ro2)) + bb * bb;
-    const double temp = -log(2.0) + log(1 + B * (1 - ro2) + safe_sqrt(t));
+    const double temp = -0x1.62e42fefa39efp-1 + log_d(1 + B * (1 - ro2) + safe_sqrt(t));
     return B * kInvPi * (1.0 / temp);
   }
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
@@ -919,7 +1038,7 @@ struct LowSmooth
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
     const double dp2 = sqnorm2(in.x + out.x, in.y + out.y);
     const double cosD = safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y));
-    const double S = pow(1.0 + B * dp2, -C);
+    const double S = pow_d(1.0 + B * dp2, -C);
     const double Q = fres.eval(cosD);
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0;
@@ -929,7 +1048,7 @@ struct LowSmooth
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
     const bool m = (component & kFlagSpecular) && (out.z > 0);
-    const double factor = (fabs(C - 1) < kEps) ? log(B + 1) / (2 * B) : (1.0 - pow(B + 1, 1 - C)) / (2 * B * (C - 1));
+    const double factor = (fabs(C - 1) < kEps) ? log_d(B + 1) / (2 * B) : (1.0 - pow_d(B + 1, 1 - C)) / (2 * B * (C - 1));
     const double q = (fres.eta - 1) / (fres.eta + 1);
     const double R0 = q * q;
 #pragma unroll
@@ -943,9 +1062,9 @@ struct LowSmooth
     const double ro2 = sin_theta2(out);
     const double bb = B * (1 - ro2);
     double temp = 1.0 + (2 * B * (1.0 + ro2)) + bb * bb;
-    temp = -log(2.0) + log(1 + B * (1 - ro2) + safe_sqrt(temp));
+    temp = -0x1.62e42fefa39efp-1 + log_d(1 + B * (1 - ro2) + safe_sqrt(temp));
     const double mdpi = B * (1.0 / temp);
-    const double E = 2.0 * exp(xi0 * B * (1.0 / mdpi));
+    const double E = 2.0 * exp_d(xi0 * B * (1.0 / mdpi));
     const double ri = safe_sqrt((E - 2) * (E + 2 * B * ro2) / (2 * E * B));
     const double ro = sqrt(ro2);
     const double rp = ri + ro, rm = ri - ro;
@@ -980,7 +1099,7 @@ struct Bagher
 {
   static constexpr int kParams = 30;
   static constexpr uint32_t kComponent = kFlagSpecular;
-  double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3];
+  double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3], inv_alpha[3];
   GGX<false> ggx;
   __device__ explicit Bagher(const double* q) : ggx(q + 18)
   {
@@ -988,12 +1107,13 @@ struct Bagher
     {
       albedo[j] = q[j]; K[j] = q[3 + j]; Lambda[j] = q[6 + j]; c[j] = q[9 + j]; theta0[j] = q[12 + j];
       k[j] = q[15 + j]; alpha[j] = q[18 + j]; p[j] = q[21 + j]; F0[j] = q[24 + j]; F1[j] = q[27 + j];
+      inv_alpha[j] = 1.0 / alpha[j];
     }
     ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
   }
   __device__ __forceinline__ double G1(int j, double th) const
   {
-    return (th > theta0[j]) ? 1.0 + Lambda[j] * (1.0 - exp(c[j] * pow(th - theta0[j], k[j]))) : 1.0;
+    return (th > theta0[j]) ? 1.0 + Lambda[j] * (1.0 - exp_d(c[j] * pow_d(th - theta0[j], k[j]))) : 1.0;
   }
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
@@ -1006,17 +1126,21 @@ struct Bagher
     const bool gmask = (inh > 0) && (outh > 0);
     const double th_in = theta_of(in), th_out = theta_of(out);
     const double cosF = 0.5 * (inh + outh);
-    const double x5 = pow(1.0 - cosF, 5.0);
+    const double x5 = pow5_d(1.0 - cosF);
+    // the quotients by per-channel constants and by the pair's common denominators as products with one
+    // reciprocal each (<= 2 ulp apart from the reference's quotients), and sgd.h:58-59's
+    // exp(-t) / pow(t, p) as one exponential e^(-t - p ln t) on log2_d (den > eps <=> p log2 t > -52)
+    const double inv_dnorm = 1.0 / dnorm, inv_cos = 1.0 / (kPi * (in.z * out.z));
 #pragma unroll
     for (int j = 0; j < 3; ++j)
     {
-      const double t = alpha[j] + tan2 / alpha[j];
-      const double den = pow(t, p[j]);
-      const double P22 = (den > kEps) ? exp(-t) / den : 0.0;
-      const double Dj = ((h.z > 0) ? P22 / dnorm : 0.0) * K[j];
+      const double t = alpha[j] + tan2 * inv_alpha[j];
+      const double lden = p[j] * log2_d(t);
+      const double P22 = (lden > -52.0) ? exp_d(-__builtin_fma(lden, 0x1.62e42fefa39efp-1, t)) : 0.0;
+      const double Dj = ((h.z > 0) ? P22 * inv_dnorm : 0.0) * K[j];
       const double Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0;
       const double Fj = (F0[j] + (1.0 - F0[j]) * x5) - F1[j] * cosF;
-      const double res = Dj * Gj * Fj / kPi / (in.z * out.z);
+      const double res = Dj * Gj * Fj * inv_cos;
       rgb[j] = active ? res * albedo[j] : 0.0;
     }
     pdf = active ? vndf_pdf(ggx, out, h, ggx.eval(h)) / (4.0 * fabs(outh)) : 0.0;
@@ -1024,7 +1148,7 @@ struct Bagher
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
     const bool m = (component & kFlagSpecular) && (out.z > 0);
-    const double x5 = pow(1.0 - out.z, 5.0);
+    const double x5 = pow5_d(1.0 - out.z);
 #pragma unroll
     for (int j = 0; j < 3; ++j) rgb[j] = m ? ((F0[j] + (1.0 - F0[j]) * x5) - F1[j] * out.z) / kPi * 4.0 * albedo[j] : 0.0;
   }
@@ -1074,14 +1198,14 @@ struct EpdNdf
   __device__ __forceinline__ double eval(d3 h) const
   {
     const double c2 = h.z * h.z;
-    const double D = normalization * exp(-pow(((1 - c2) / c2) / (beta * beta), p)) / (c2 * c2);
+    const double D = normalization * exp_d(-pow_d(((1 - c2) / c2) / (beta * beta), p)) / (c2 * c2);
     return (h.z > 0) ? D : 0.0;
   }
   // G1.h:14-16 index maps, then the bilinear interpolation of the clamped floor / ceil entries
   __device__ __forceinline__ double lookup(double t) const
   {
     const double m0 = 5.0 / p - 1.0;
-    const double m1 = exp(-exp(log(1.0 / t) * 0.05)) * 1000.0 - 1.0;
+    const double m1 = exp_d(-exp_d(log_d(1.0 / t) * 0.05)) * 1000.0 - 1.0;
     auto at = [&](double i0, double i1) {
       const int r = int(fmin(fmax(i0, 0.0), 99.0)), c = int(fmin(fmax(i1, 0.0), 999.0));
       return double(tab[r * 1000 + c]);
@@ -1112,7 +1236,7 @@ struct EpdNdf
     // xi1 = 1: the reference's gamma_q_inv(a, q = 1) starts its Halley iteration at p = 0, x = 0, where
     // t = (P - p) / R(a, 0) = 0 / 0 (util/invgamma.h:404-414): its sampled normal is NaN, and so is this one
     const double g = (xi1 >= 1.0) ? __builtin_nan("") : gamma_q_inv_d(inv_p, xi1);
-    const double tan2 = beta * beta * pow(g, inv_p);
+    const double tan2 = beta * beta * pow_d(g, inv_p);
     const double cosT = 1.0 / sqrt(1.0 + tan2);
     const double sinT = safe_sqrt(1.0 - cosT * cosT);
     return mk(cp * sinT, sp * sinT, cosT);
@@ -1250,7 +1374,7 @@ struct He
     const double scot = tau * (1.0 / tan_theta(v)) / (2.0 * sigma0);
     const double ec = 0.5 * erfc(scot);
     double lambda = 0.5 * kInvSqrtPi / scot;
-    if (ERRATA) lambda *= exp(-(scot * scot));
+    if (ERRATA) lambda *= exp_d(-(scot * scot));
     lambda -= ec;
     return (sigma0 < kEps) ? 1.0 : (1.0 - ec) / (lambda + 1.0);
   }
@@ -1276,10 +1400,10 @@ struct He
     auto K = [&](double t) { return t * erfc(tau / (2 * sigma0 * t)); };
     const double Ki = (ti > kEps) ? K(ti) : 0.0, Ko = (to > kEps) ? K(to) : 0.0;
     const double f0 = (1.0 / sqrt(8.0 * kPi)) * (Ki + Ko);
-    double x = (f0 <= 1.0) ? f0 : safe_sqrt(2.0 * log(f0));
+    double x = (f0 <= 1.0) ? f0 : safe_sqrt(2.0 * log_d(f0));
     for (int s = 0; s < 4; ++s)
     {
-      const double expn = exp(0.5 * x * x);
+      const double expn = exp_d(0.5 * x * x);
       const double ev = x * expn - f0, grad = (1 + x * x) * expn;
       x -= (grad > kEps) ? ev / grad : 0.0;
     }
@@ -1305,7 +1429,7 @@ struct He
     double rough[3] = {0.0, 0.0, 0.0}, weight = 0.0;
     if (APPROX >= 0 && gmin > double(APPROX))
     {
-      for (int c = 0; c < 3; ++c) rough[c] = exp(-eb[c] / g[c]) / g[c];
+      for (int c = 0; c < 3; ++c) rough[c] = exp_d(-eb[c] / g[c]) / g[c];
       weight = fmin(fmax(gmin - double(APPROX), 0.0), 1.0);
     }
     double sum[3] = {0.0, 0.0, 0.0}, gm[3] = {1.0, 1.0, 1.0}, term[3] = {0.0, 0.0, 0.0}, last[3];
@@ -1317,7 +1441,7 @@ struct He
       {
         last[c] = term[c];
         gm[c] *= g[c] / m;
-        term[c] = exp(-g[c] - eb[c] / m) * gm[c] / m;
+        term[c] = exp_d(-g[c] - eb[c] / m) * gm[c] / m;
         sum[c] += term[c];
       }
       if (ADAPTIVE)

@@ -327,8 +327,14 @@ struct He
 #ifdef BBM_HIP_HE_PROBE_NO_SERIES
     converged = true;       // timing probe only (tools/build_variant.sh): the prelude without the series
 #endif
+#ifdef BBM_HIP_HE_COUNT_TERMS
+    int nterms = 0;         // diagnostics build only (tools/he_terms.py): D = (terms run, length key, 0)
+#endif
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
+#ifdef BBM_HIP_HE_COUNT_TERMS
+      nterms = m;
+#endif
       const double rm = inv_small(m);
       const float mf = float(m), rmf = float(rm);
       double ex[3];
@@ -385,6 +391,9 @@ struct He
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], d.rough[c], weight)));
+#ifdef BBM_HIP_HE_COUNT_TERMS
+    Dout[0] = float(nterms); Dout[1] = float(D_key(d)); Dout[2] = 0.0f;
+#endif
   }
 
   __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
@@ -428,6 +437,9 @@ struct He
       float v = e.pre[c] * Dv[c];
       if (SCALED && SCALE) v *= albedo[c];
       rgb[c] = e.active ? v : 0.0f;
+#ifdef BBM_HIP_HE_COUNT_TERMS
+      rgb[c] = Dv[c];
+#endif
     }
   }
 
@@ -461,8 +473,13 @@ struct He
 
   // the compaction kernel's two-phase evaluation (kernels.hpp): stage 1 everything but the series, with its
   // length key; stage 2 the series and the product -- the same operations as eval_pdf, split at the series
+  // measured per model (tools/gpu_r03_e.sh, config 3, ms per 10 M pairs, one-phase -> two-phase): He 0.737 ->
+  // 0.671, HeWestin 1.153 -> 1.152, NganHe 1.089 -> 1.088, HeHolzschuch (10 fixed terms: nothing to sort)
+  // 0.390 -> 0.406; on for the adaptive series only
 #ifndef BBM_HIP_HE_ONEPHASE
-  static constexpr bool kTwoPhase = true;
+  static constexpr bool kTwoPhase = ADAPTIVE;
+#else
+  static constexpr bool kTwoPhase = false;
 #endif
   struct Stage { EvalPrep e; float pdf; };
   static constexpr int kStageWords = 14;

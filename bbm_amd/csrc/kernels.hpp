@@ -324,7 +324,7 @@ inline bool use_compact()
 constexpr int kSortBuckets = 32;
 template<class Model, int MODE> constexpr bool two_phase()
 {
-  if constexpr (requires { Model::kTwoPhase; }) return (MODE & kModeEval) != 0;
+  if constexpr (requires { Model::kTwoPhase; }) return Model::kTwoPhase && (MODE & kModeEval) != 0;
   else return false;
 }
 template<class Model> constexpr int stage_words()

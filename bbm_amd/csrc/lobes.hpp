@@ -77,7 +77,7 @@ struct Ward
       if (KIND == 0) nf = kPi4F * sqrtf(in.z * out.z) * rx * ry;
       else if (KIND == 1) nf = kPi4F * rx * ry * (in.z * out.z);
       else nf = f_div_d(double(kPi4F * rx * ry) * (double(zH2) * double(zH2)), double(dot3(H, H)));
-      const float f = div_nr(expf_dn(-exponent), nf);
+      const float f = div_nr(expf_lobe(-exponent), nf);
       rgb[0] = active ? albedo[0] * f : 0.0f;
       rgb[1] = active ? albedo[1] * f : 0.0f;
       rgb[2] = active ? albedo[2] * f : 0.0f;
@@ -88,7 +88,7 @@ struct Ward
       const v3 h = halfway(in, out);
       const float nf = kPi4F * rx * ry * dot3(in, h) * cube_f(h.z);
       const float exponent = div_nr(sqnorm2(div_nr(h.x, rx), div_nr(h.y, ry)), h.z * h.z);
-      const float p = div_nr(expf_dn(-exponent), nf);
+      const float p = div_nr(expf_lobe(-exponent), nf);
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;

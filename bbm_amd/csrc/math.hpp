@@ -214,6 +214,19 @@ __device__ __forceinline__ float expf_glibc(float x)
   // |x| >= 88 or NaN in glibc: -inf and x < log(2^-150) -> 0, x > log(2^128) -> inf, NaN -> NaN (via res)
   return (x < -0x1.9fe368p6f) ? 0.0f : ((x > 0x1.62e42ep6f) ? __builtin_inff() : res);
 }
+// the exponential of the eval kernels' Gaussian-like lobes (Ward, EPD; -DBBM_HIP_LOBES_EXP_DN: the 1.4-ulp
+// expf_dn, A/B).  Measured against expf_dn (tools/gpu_r03_e.sh, ms per 10 M pairs / bit-exact lanes): Ward
+// 0.060 -> 0.060 ms, 97.0 -> 99.7 %; EPD 0.270 -> 0.285 ms, 80.1 -> 83.5 %
+__device__ __forceinline__ float expf_glibc_neg(float x);
+__device__ __forceinline__ float expf_lobe(float x)
+{
+#ifdef BBM_HIP_LOBES_EXP_DN
+  return expf_dn(x);
+#else
+  return expf_glibc_neg(x);
+#endif
+}
+
 // the same for x <= 0 or NaN (an exponent that is minus a square or a quotient of squares): no overflow select
 __device__ __forceinline__ float expf_glibc_neg(float x)
 {

@@ -77,11 +77,13 @@ struct Beckmann
     {
       const float slope = erfinv_s(x);
       const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_dn(-slope * slope) - xc0);
-      const float der = float(1.0 - slope * tanT);
+      // float(1.0 - p) of a float p: one double op on float operands rounded to float is the float op itself
+      // (53 >= 2 x 24 + 2), so the f32 subtraction -- likewise 2 xc1 - 1 below (2 xc1 exact in either type)
+      const float der = 1.0f - slope * tanT;
       x -= div_nr(val, der);
     }
     float s0 = 0.0f, s1 = 0.0f;
-    if (x > -1.0 && x < +1.0) { s0 = erfinv_s(x); s1 = erfinv_s(float(2.0 * xc1 - 1.0)); }
+    if (x > -1.0 && x < +1.0) { s0 = erfinv_s(x); s1 = erfinv_s(2.0f * xc1 - 1.0f); }
     float c, s;
     cossin_phi(vs, c, s);
     const float u0 = ((0.0f + c * s0) + -s * s1) * au;

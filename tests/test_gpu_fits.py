@@ -47,12 +47,13 @@ def test_every_published_material_matches_reference(bbm, fname):
         ref = ou.oracle_eval_pdf(key, p, pin, pout, nthreads=8)
         provers = [tp._input_ulps_prover(lambda a, b: ou.oracle_eval_pdf(key, p, a, b, nthreads=8), [pin, pout], got),
                    tp._libm_prover(lambda a, b: ou.oracle_eval_pdf(key, p, a, b, nthreads=1), [pin, pout], got)]
-        st = tp.check_lanes(got, ref, f"{fname}:{mat} eval+pdf", provers)
+        st = tp.check_lanes(got, ref, f"{fname}:{mat} eval+pdf", provers, model=key)
         refl = m.reflectance(tp._dev(sout)).cpu().numpy()
         rr = ou.ref_reflectance(key, p, sout)
         tp.check_lanes(refl, rr, f"{fname}:{mat} reflectance",
-                       [tp._input_ulps_prover(lambda o: ou.ref_reflectance(key, p, o), [sout], refl)])
-        stats[mat] = {k: st[k] for k in ("max_rel_normal", "frac_bit_exact", "lanes_outside_bar", "proven_by")}
+                       [tp._input_ulps_prover(lambda o: ou.ref_reflectance(key, p, o), [sout], refl)], model=key)
+        stats[mat] = {k: st[k] for k in ("max_rel_normal", "max_rel_proven", "frac_bit_exact", "lanes_outside_bar",
+                                         "proven_by")}
         n_mat += 1
     assert n_mat == sum(1 for x in FITS[fname] if x[3] is not None)
     tp._report("fits_" + fname.replace(".fit", ""), {

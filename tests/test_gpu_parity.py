@@ -35,6 +35,13 @@ INP = ou.golden_inputs()
 TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
 MAX_EXCUSED_FRAC = 1e-3       # at most this fraction of a batch's lanes may need an input-ulps proof
 MAX_SAMPLER_FRAC = 0.05       # ... a sampler-CDF proof (a CDF entry moves the ~2/90 of directions in its bins)
+# Ceiling on the relative error of the lanes that pass by a proof (the proofs bound WHY a lane differs, this bounds
+# HOW MUCH): the ill-conditioned lanes of the cancelling models -- Bagher's shadowing 1 + Lambda (1 - e^(c t^k))
+# and the He family's series at tiny D -- reach ~1e-2 at their fitted parameters (profiles/r02_parity_large_0*.json);
+# every other model stays below 1e-3.  A kernel regression confined to ill-conditioned lanes would exceed these.
+EXCUSED_REL_CEILING = {"Bagher": 5e-2, "Aggregate<Lambertian,Bagher>": 5e-2, "He": 2e-2, "HeWestin": 2e-2,
+                       "HeHolzschuch": 2e-2, "NganHe": 2e-2, "Aggregate<Lambertian,NganHe>": 2e-2}
+EXCUSED_REL_DEFAULT = 1e-3
 
 
 @pytest.fixture(scope="module")
@@ -69,9 +76,10 @@ def _report(tag, stats):
         print(f"{tag} {k}: {v}")
 
 
-def check_lanes(got, ref, what, provers=()):
+def check_lanes(got, ref, what, provers=(), model=None):
     """Apply the per-lane bar to (channels, lanes) arrays; lanes outside it must be proven by one of `provers`
-    (functions lanes -> bool array); returns the statistics reported under gpurun_out/parity_*.json."""
+    (functions lanes -> bool array), and even a proven lane must stay within the model's EXCUSED_REL_CEILING
+    (`model`, default: the name `what` starts with); returns the statistics reported under gpurun_out/parity_*.json."""
     got = np.asarray(got)
     ref = np.asarray(ref)
     n = got.shape[-1]
@@ -93,8 +101,11 @@ def check_lanes(got, ref, what, provers=()):
     assert bad.size - n_sampler <= max(2, MAX_EXCUSED_FRAC * n), \
         f"{what}: {bad.size - n_sampler} of {n} lanes needed an input-ulps proof ({proven})"
     assert n_sampler <= max(2, MAX_SAMPLER_FRAC * n), f"{what}: {n_sampler} of {n} lanes needed a sampler-CDF proof"
+    excused = ou.max_rel_normal(got[..., bad], ref[..., bad]) if bad.size else 0.0
+    ceiling = EXCUSED_REL_CEILING.get(model or what.split("[")[0].split(" ")[0].split("/")[0], EXCUSED_REL_DEFAULT)
+    assert excused <= ceiling, f"{what}: a proven lane is {excused:.3e} off (ceiling {ceiling:g})"
     sub = (np.abs(ref) < ou.FLT_MIN) & (ref != 0)
-    return {"lanes": int(n), "max_rel_normal": ou.max_rel_normal(got, ref),
+    return {"lanes": int(n), "max_rel_normal": ou.max_rel_normal(got, ref), "max_rel_proven": excused,
             "max_ulp": int(ou.ulp_diff(got, ref).max()) if got.size else 0,
             "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0)) if got.size else 1.0,
             "subnormal_ref_values": int(sub.sum()), "lanes_outside_bar": int(bad.size),
