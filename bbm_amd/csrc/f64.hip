@@ -37,8 +37,9 @@ __device__ __forceinline__ void st(double* p, uint64_t t, const double* v)
   else __builtin_nontemporal_store(v[0], p + t);
 }
 
-template<class Model, int V, bool MASK>
-__global__ __launch_bounds__(kBlock) void k_eval_pdf_f64(EvalArgsF64 a)
+// W: minimum waves per SIMD (amdgpu_waves_per_eu; 1 = no constraint)
+template<class Model, int V, bool MASK, int W = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_eval_pdf_f64(EvalArgsF64 a)
 {
   const Model m(a.p.v);
   const uint64_t nv = a.n / V;
@@ -113,6 +114,10 @@ int launched(const char* what)
 // Grid cap (0 = full grid): the Student-T NDF's per-thread setup (two f64 tgamma and a pow) is amortised over
 // several grid-stride iterations (the floatRGB kernels' eval_grid_cap, kernels.hpp)
 template<class Model> struct grid_cap { static constexpr unsigned value = 0; };
+#ifndef BBM_HIP_F64_HEAVY_WAVES
+#define BBM_HIP_F64_HEAVY_WAVES 2
+#endif
+constexpr int kHeavyWaves = BBM_HIP_F64_HEAVY_WAVES;
 template<> struct grid_cap<RibardiereM> { static constexpr unsigned value = 2048; };
 template<> struct grid_cap<RibardiereAnisoM> { static constexpr unsigned value = 2048; };
 
@@ -212,6 +217,14 @@ int launch_eval_pdf(const EvalArgsF64& a0, hipStream_t s)
                   aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
   unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
   if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
+  if constexpr (heavy_f64<Model>())
+  {
+    // one pair per thread with an occupancy floor: see heavy_f64 (f64.hpp)
+    blocks = grid(a.n);
+    if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true, kHeavyWaves>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, false, kHeavyWaves>), dim3(blocks), dim3(kBlock), 0, s, a);
+    return launched("k_eval_pdf_f64");
+  }
   if (v2 && a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (v2) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true>), dim3(blocks), dim3(kBlock), 0, s, a);

@@ -23,6 +23,14 @@ constexpr double kEps = 2.220446049250313080847263336181640625e-16;   // numeric
 constexpr double kPi = 3.141592653589793115997963468544185161590576171875;          // std::numbers::pi (double)
 constexpr double kInvPi = 0.31830988618379069121644420192751567810773849487304688;  // std::numbers::inv_pi
 
+// models whose doubleRGB evaluation is a long f64 computation (the He family's prelude and series): launched one
+// pair per thread with an occupancy floor (f64.hip), where two pairs per thread took ~290 VGPRs (1 wave per SIMD)
+template<class M> constexpr bool heavy_f64()
+{
+  if constexpr (requires { M::kHeavyF64; }) return M::kHeavyF64;
+  else return false;
+}
+
 struct d3 { double x, y, z; };
 __device__ __forceinline__ d3 mk(double x, double y, double z) { return d3{x, y, z}; }
 __device__ __forceinline__ double dot(d3 a, d3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
@@ -647,6 +655,7 @@ struct Aggregate
 {
   static constexpr int kParams = A::kParams + B::kParams;
   static constexpr uint32_t kComponent = A::kComponent | B::kComponent;
+  static constexpr bool kHeavyF64 = heavy_f64<A>() || heavy_f64<B>();
   A a;
   B b;
   __device__ explicit Aggregate(const double* p) : a(p), b(p + A::kParams) {}
@@ -1099,7 +1108,7 @@ struct Bagher
 {
   static constexpr int kParams = 30;
   static constexpr uint32_t kComponent = kFlagSpecular;
-  double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3], inv_alpha[3];
+  double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3], inv_alpha[3], hc0[3], hc_min;
   GGX<false> ggx;
   __device__ explicit Bagher(const double* q) : ggx(q + 18)
   {
@@ -1108,12 +1117,27 @@ struct Bagher
       albedo[j] = q[j]; K[j] = q[3 + j]; Lambda[j] = q[6 + j]; c[j] = q[9 + j]; theta0[j] = q[12 + j];
       k[j] = q[15 + j]; alpha[j] = q[18 + j]; p[j] = q[21 + j]; F0[j] = q[24 + j]; F1[j] = q[27 + j];
       inv_alpha[j] = 1.0 / alpha[j];
+      // theta > theta0 <=> 2 asin(c) > theta0 <=> c > sin(theta0 / 2) for the half chord c of theta_of (asin is
+      // increasing; both sides round, so only lanes within an ulp of the boundary can decide differently, where
+      // G1 = 1 + Lambda (1 - e^(c 0^k)) = 1 on either side)
+      hc0[j] = (theta0[j] <= 0.0) ? -1.0 : ((theta0[j] >= kPi) ? 2.0 : sin(0.5 * theta0[j]));
     }
+    hc_min = fmin(fmin(hc0[0], hc0[1]), hc0[2]);
     ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
   }
-  __device__ __forceinline__ double G1(int j, double th) const
+  // sgd.h:185-190 G1 for an upper-hemisphere direction with half chord hc (theta = 2 asin(hc)): the branch skips the shadowing
+  // term (a log and two exponentials) where theta <= theta0; th is theta_of(v), evaluated only if some channel
+  // needs it
+  __device__ __forceinline__ double G1h(int j, double hc, double th) const
   {
-    return (th > theta0[j]) ? 1.0 + Lambda[j] * (1.0 - exp_d(c[j] * pow_d(th - theta0[j], k[j]))) : 1.0;
+    double g = 1.0;
+    if (hc > hc0[j]) g = 1.0 + Lambda[j] * (1.0 - exp_d(c[j] * pow_d(th - theta0[j], k[j])));
+    return g;
+  }
+  __device__ __forceinline__ static double half_chord(d3 v)
+  {
+    const double dz = v.z - 1.0;
+    return 0.5 * sqrt(((0.0 + v.x * v.x) + v.y * v.y) + dz * dz);
   }
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
@@ -1124,7 +1148,11 @@ struct Bagher
     const double z2 = h.z * h.z;
     const double dnorm = kPi * (z2 * z2);
     const bool gmask = (inh > 0) && (outh > 0);
-    const double th_in = theta_of(in), th_out = theta_of(out);
+    // in.z, out.z > 0 wherever the result is used: theta_of = 2 asin(half chord)
+    const double hc_in = half_chord(in), hc_out = half_chord(out);
+    double th_in = 0.0, th_out = 0.0;
+    if (hc_in > hc_min) th_in = theta_of(in);
+    if (hc_out > hc_min) th_out = theta_of(out);
     const double cosF = 0.5 * (inh + outh);
     const double x5 = pow5_d(1.0 - cosF);
     // the quotients by per-channel constants and by the pair's common denominators as products with one
@@ -1138,7 +1166,7 @@ struct Bagher
       const double lden = p[j] * log2_d(t);
       const double P22 = (lden > -52.0) ? exp_d(-__builtin_fma(lden, 0x1.62e42fefa39efp-1, t)) : 0.0;
       const double Dj = ((h.z > 0) ? P22 * inv_dnorm : 0.0) * K[j];
-      const double Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0;
+      const double Gj = gmask ? G1h(j, hc_in, th_in) * G1h(j, hc_out, th_out) : 0.0;
       const double Fj = (F0[j] + (1.0 - F0[j]) * x5) - F1[j] * cosF;
       const double res = Dj * Gj * Fj * inv_cos;
       rgb[j] = active ? res * albedo[j] : 0.0;
@@ -1356,6 +1384,7 @@ struct He
   static constexpr int kOff = SCALED ? 3 : 0;
   static constexpr int kParams = kOff + 2 + FRES::kParams;
   static constexpr uint32_t kComponent = kFlagSpecular;
+  static constexpr bool kHeavyF64 = true;
   double albedo[3], sigma0, tau;
   FRES fres;
   const double* cdf;
@@ -1455,9 +1484,16 @@ struct He
     // (a 9-FMA polynomial, ~2^-44 relative) instead of the library's double exp (~40 instructions), and the
     // divisions by m as products with 1/m (a table): each term within ~1e-13 of the reference's, far inside the
     // 1e-9 the doubleRGB tests hold the He family to.
-    double eg[3];
+#ifdef BBM_HIP_HE_PROBE_NO_SERIES
+    converged = true;       // timing probe only (tools/build_variant.sh): the prelude without the series
+#endif
+    double eg[3], cap[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) eg[c] = converged ? 0.0 : exp_dd(fmax(-g[c], -1.0e4));
+    for (int c = 0; c < 3; ++c)
+    {
+      eg[c] = converged ? 0.0 : exp_dd(fmax(-g[c], -1.0e4));
+      cap[c] = (ADAPTIVE && !converged) ? eg[c] * exp_dd(fmax(-eb[c] * (1.0 / 64.0), -1.0e4)) * (1.0 + 0x1p-30) : 0.0;
+    }
     for (int m = 1; m <= TAYLOR && !converged; ++m)
     {
       const double rm = inv_small(m);
@@ -1490,7 +1526,7 @@ struct He
 #pragma unroll
           for (int c = 0; c < 3; ++c)
           {
-            const double bound = eg[c] * exp_dd(fmax(-eb[c] * (1.0 / 64.0), -1.0e4)) * gm[c] * rm * (1.0 + 0x1p-30);
+            const double bound = cap[c] * gm[c] * rm;     // cap = e^(-g) e^(-eb/64) (1 + 2^-30), loop-invariant
             // 2 bound < ulp(sum): the ulp of a normal sum is 2^(ilogb - 52), of a zero or subnormal one 2^-1074
             const int e = (sum[c] > 0.0) ? max(__builtin_amdgcn_frexp_exp(sum[c]) - 53, -1074) : -1074;   // frexp exponent = ilogb + 1
             settled = settled && (double(m) + 1.0 >= g[c]) && (2.0 * bound < __builtin_ldexp(1.0, e));

@@ -392,7 +392,11 @@ struct He
 #pragma unroll
     for (int c = 0; c < 3; ++c) Dout[c] = float(norm[c] * double(std_lerpf(sum[c], d.rough[c], weight)));
 #ifdef BBM_HIP_HE_COUNT_TERMS
+#if BBM_HIP_HE_COUNT_TERMS == 2
+    Dout[0] = float(nterms); Dout[1] = float(g[1]); Dout[2] = eb[1];     // (terms, g, eb) of the green channel
+#else
     Dout[0] = float(nterms); Dout[1] = float(D_key(d)); Dout[2] = 0.0f;
+#endif
 #endif
   }
 

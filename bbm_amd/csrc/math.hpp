@@ -64,10 +64,28 @@ __device__ __forceinline__ float div_nr(float n, float d)
   const float q = n * r;
   const float e = __builtin_fmaf(-d, q, n);
   const float q1 = __builtin_fmaf(e, r, q);
+#ifdef BBM_HIP_DIV_SUB
+  // q1 is the correctly rounded quotient where numerator and quotient are normal floats (or n = 0).  A subnormal
+  // numerator or quotient rounds the remainder e to the subnormal grid, so the correction can be off by an ulp
+  // there: those lanes (a wave-uniform branch, taken only when some lane needs it) divide in double with one f64
+  // remainder step (f_div_d), rounded once to float -- the IEEE quotient on the subnormal grid as well.
+  const bool fast = (__builtin_isnormal(q1) && __builtin_isnormal(n)) || n == 0.0f;
+  float res = q1;
+  if (__builtin_amdgcn_ballot_w64(!fast) != 0)
+  {
+    const double dd = double(d), nd = double(n);
+    const double q0 = double(q);
+    const double qd = __builtin_fma(__builtin_fma(-dd, q0, nd), double(r), q0);
+    const float s = __builtin_isfinite(qd) ? float(qd) : q;      // d = 0 / inf, n = inf, NaN: IEEE result q
+    res = fast ? q1 : s;
+  }
+  return res;
+#else
   // q1 is the corrected quotient only where it is a normal float: for a subnormal quotient the remainder e is
   // itself rounded to the subnormal grid and the "correction" can move a correctly rounded q (n * rcp(d), within
   // ~1e-7 relative) off by an ulp; q is kept there, and for the IEEE special cases (inf, NaN, 0) as before.
   return __builtin_isnormal(q1) ? q1 : q;
+#endif
 }
 
 // a / d for the quotients that are a normal float or exactly 0 on every lane whose result is used (a finite
@@ -382,7 +400,20 @@ __device__ __forceinline__ float div_ff(float nh, float nl, float dh, float dl)
   q = __builtin_fmaf(__builtin_fmaf(-dh, q, nh), r, q);           // ~correctly rounded nh / dh
   const float rem = __builtin_fmaf(-dh, q, nh) + __builtin_fmaf(-q, dl, nl);
   const float q1 = __builtin_fmaf(rem, r, q);
+#ifdef BBM_HIP_DIV_SUB
+  // subnormal numerator or quotient (see div_nr): the pair quotient in double (both pair sums are exact doubles),
+  // rounded once to float, on a wave-uniform branch
+  const bool fast = (__builtin_isnormal(q1) && __builtin_isnormal(nh)) || (nh == 0.0f && nl == 0.0f);
+  float res = q1;
+  if (__builtin_amdgcn_ballot_w64(!fast) != 0)
+  {
+    const float s = float((double(nh) + double(nl)) / (double(dh) + double(dl)));
+    res = fast ? q1 : s;
+  }
+  return res;
+#else
   return __builtin_isnormal(q1) ? q1 : nh * r;     // subnormal / special results: see div_nr
+#endif
 }
 
 // horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2

@@ -24,7 +24,7 @@ def main():
         f64 = [i for i in valu if 'f64' in i]
         trans = [i for i in valu if re.match(r'v_(exp|log|rcp|rsq|sqrt|sin|cos)_', i)]
         br = [i for i in ins if i.startswith('s_cbranch')]
-        meta = re.search(re.escape(name) + r'.*?\.vgpr_count:\s+(\d+)', s, re.S)
+        meta = re.search(r'\.name:\s+' + re.escape(name) + r'\s.*?\.vgpr_count:\s+(\d+)', s, re.S)
         spill = sum(1 for i in ins if i.startswith('scratch_store') or i.startswith('buffer_store'))
         print(f"{len(ins):6d} ins {len(valu):6d} valu {len(f64):5d} f64 {len(trans):4d} trans {len(br):3d} br "
               f"vgpr {meta.group(1) if meta else '?':>4} spill {spill:3d}  {name[:110]}")
