@@ -114,10 +114,7 @@ int launched(const char* what)
 // Grid cap (0 = full grid): the Student-T NDF's per-thread setup (two f64 tgamma and a pow) is amortised over
 // several grid-stride iterations (the floatRGB kernels' eval_grid_cap, kernels.hpp)
 template<class Model> struct grid_cap { static constexpr unsigned value = 0; };
-#ifndef BBM_HIP_F64_HEAVY_WAVES
-#define BBM_HIP_F64_HEAVY_WAVES 2
-#endif
-constexpr int kHeavyWaves = BBM_HIP_F64_HEAVY_WAVES;
+
 template<> struct grid_cap<RibardiereM> { static constexpr unsigned value = 2048; };
 template<> struct grid_cap<RibardiereAnisoM> { static constexpr unsigned value = 2048; };
 
@@ -217,16 +214,19 @@ int launch_eval_pdf(const EvalArgsF64& a0, hipStream_t s)
                   aligned16(a.oz) && aligned16(a.r) && aligned16(a.g) && aligned16(a.b) && aligned16(a.pdf);
   unsigned blocks = grid(v2 ? (a.n + 1) / 2 : a.n);
   if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
-  if constexpr (heavy_f64<Model>())
+  if constexpr (heavy_f64<Model>() > 0)
   {
     // one pair per thread with an occupancy floor: see heavy_f64 (f64.hpp)
+    constexpr int W = heavy_f64<Model>();
     blocks = grid(a.n);
-    if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true, kHeavyWaves>), dim3(blocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, false, kHeavyWaves>), dim3(blocks), dim3(kBlock), 0, s, a);
+    if (grid_cap<Model>::value && blocks > grid_cap<Model>::value) blocks = grid_cap<Model>::value;
+    if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true, W>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, false, W>), dim3(blocks), dim3(kBlock), 0, s, a);
     return launched("k_eval_pdf_f64");
   }
-  if (v2 && a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, true>), dim3(blocks), dim3(kBlock), 0, s, a);
-  else if (v2) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+  constexpr int F = floor_f64<Model>();
+  if (v2 && a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, true, F>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (v2) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 2, false, F>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.mask) hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_f64<Model, 1, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   return launched("k_eval_pdf_f64");

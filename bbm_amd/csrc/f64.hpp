@@ -23,12 +23,19 @@ constexpr double kEps = 2.220446049250313080847263336181640625e-16;   // numeric
 constexpr double kPi = 3.141592653589793115997963468544185161590576171875;          // std::numbers::pi (double)
 constexpr double kInvPi = 0.31830988618379069121644420192751567810773849487304688;  // std::numbers::inv_pi
 
-// models whose doubleRGB evaluation is a long f64 computation (the He family's prelude and series): launched one
-// pair per thread with an occupancy floor (f64.hip), where two pairs per thread took ~290 VGPRs (1 wave per SIMD)
-template<class M> constexpr bool heavy_f64()
+// models whose doubleRGB evaluation is a long f64 computation (the He family's prelude and series, Bagher): launched
+// one pair per thread with an occupancy floor of kF64Waves waves per SIMD (f64.hip), where two pairs per thread took
+// ~290 VGPRs for He (1 wave per SIMD).  0: the default launch (two pairs per thread, no floor).
+template<class M> constexpr int heavy_f64()
 {
-  if constexpr (requires { M::kHeavyF64; }) return M::kHeavyF64;
-  else return false;
+  if constexpr (requires { M::kF64Waves; }) return M::kF64Waves;
+  else return 0;
+}
+// an occupancy floor for the default two-pairs-per-thread launch (1: none)
+template<class M> constexpr int floor_f64()
+{
+  if constexpr (requires { M::kF64Floor; }) return M::kF64Floor;
+  else return 1;
 }
 
 struct d3 { double x, y, z; };
@@ -127,6 +134,11 @@ __device__ __forceinline__ double log2_d(double x)
   return double(k) + __builtin_fma(l1p, 0x1.71547652b82fep0, double(l0));
 }
 
+// the device library's f64 exp: measured faster than exp_d inside the He family's prelude (He 1.50 -> 1.47,
+// HeHolzschuch 0.80 -> 0.75 ms per 10 M pairs; exp_d is faster in the microfacet models: CookTorrance 0.158 ->
+// 0.150), where the kernel runs at its 256-VGPR cap
+__device__ __forceinline__ double exp_lib(double a) { return exp(a); }
+
 // glibc's log restated on log2_d (x < 0 -> NaN; x = 0 -> -inf; inf -> inf; NaN -> NaN)
 __device__ __forceinline__ double log_d(double x)
 {
@@ -211,12 +223,12 @@ template<bool Aniso, bool Normalize>
 struct Beckmann
 {
   static constexpr int kParams = Aniso ? 2 : 1;
-  double au, av;
-  __device__ explicit Beckmann(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]) {}
+  double au, av, iau, iav;     // 1 / alpha: the per-pair quotients by the roughness as products (<= 1 ulp apart)
+  __device__ explicit Beckmann(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]), iau(1.0 / au), iav(1.0 / av) {}
   __device__ __forceinline__ double eval(d3 h) const
   {
     const double c2 = h.z * h.z;
-    double D = exp_d(-sqnorm2(h.x / au, h.y / av) / c2) / (au * av * c2 * c2);
+    double D = exp_d(-sqnorm2(h.x * iau, h.y * iav) / c2) / (au * av * c2 * c2);
     if (Normalize) D *= kInvPi;
     return (h.z > 0) ? D : 0.0;
   }
@@ -258,11 +270,11 @@ template<bool Aniso>
 struct GGX
 {
   static constexpr int kParams = Aniso ? 2 : 1;
-  double au, av;
-  __device__ explicit GGX(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]) {}
+  double au, av, iau, iav;     // 1 / alpha (as Beckmann)
+  __device__ explicit GGX(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]), iau(1.0 / au), iav(1.0 / av) {}
   __device__ __forceinline__ double eval(d3 h) const
   {
-    const double s = sqnorm2(h.x / au, h.y / av) + h.z * h.z;
+    const double s = sqnorm2(h.x * iau, h.y * iav) + h.z * h.z;
     const double D = 1.0 / (kPi * (au * av) * (s * s));
     return (h.z > 0) ? D : 0.0;
   }
@@ -655,7 +667,7 @@ struct Aggregate
 {
   static constexpr int kParams = A::kParams + B::kParams;
   static constexpr uint32_t kComponent = A::kComponent | B::kComponent;
-  static constexpr bool kHeavyF64 = heavy_f64<A>() || heavy_f64<B>();
+  static constexpr int kF64Waves = heavy_f64<A>() > heavy_f64<B>() ? heavy_f64<A>() : heavy_f64<B>();
   A a;
   B b;
   __device__ explicit Aggregate(const double* p) : a(p), b(p + A::kParams) {}
@@ -1108,6 +1120,9 @@ struct Bagher
 {
   static constexpr int kParams = 30;
   static constexpr uint32_t kComponent = kFlagSpecular;
+#ifdef BBM_HIP_F64_BAGHER_FLOOR
+  static constexpr int kF64Floor = BBM_HIP_F64_BAGHER_FLOOR;   // A/B: two pairs per thread, an occupancy floor
+#endif
   double albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3], inv_alpha[3], hc0[3], hc_min;
   GGX<false> ggx;
   __device__ explicit Bagher(const double* q) : ggx(q + 18)
@@ -1124,6 +1139,7 @@ struct Bagher
     }
     hc_min = fmin(fmin(hc0[0], hc0[1]), hc0[2]);
     ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
+    ggx.iau = ggx.iav = 1.0 / ggx.au;
   }
   // sgd.h:185-190 G1 for an upper-hemisphere direction with half chord hc (theta = 2 asin(hc)): the branch skips the shadowing
   // term (a log and two exponentials) where theta <= theta0; th is theta_of(v), evaluated only if some channel
@@ -1384,7 +1400,10 @@ struct He
   static constexpr int kOff = SCALED ? 3 : 0;
   static constexpr int kParams = kOff + 2 + FRES::kParams;
   static constexpr uint32_t kComponent = kFlagSpecular;
-  static constexpr bool kHeavyF64 = true;
+#ifndef BBM_HIP_F64_HE_WAVES
+#define BBM_HIP_F64_HE_WAVES 2     // one pair per thread, <= 256 VGPRs: He 2.22 -> 1.49 ms per 10 M pairs (3 / 4: slower)
+#endif
+  static constexpr int kF64Waves = BBM_HIP_F64_HE_WAVES;
   double albedo[3], sigma0, tau;
   FRES fres;
   const double* cdf;
@@ -1403,7 +1422,7 @@ struct He
     const double scot = tau * (1.0 / tan_theta(v)) / (2.0 * sigma0);
     const double ec = 0.5 * erfc(scot);
     double lambda = 0.5 * kInvSqrtPi / scot;
-    if (ERRATA) lambda *= exp_d(-(scot * scot));
+    if (ERRATA) lambda *= exp_lib(-(scot * scot));
     lambda -= ec;
     return (sigma0 < kEps) ? 1.0 : (1.0 - ec) / (lambda + 1.0);
   }
@@ -1432,7 +1451,7 @@ struct He
     double x = (f0 <= 1.0) ? f0 : safe_sqrt(2.0 * log_d(f0));
     for (int s = 0; s < 4; ++s)
     {
-      const double expn = exp_d(0.5 * x * x);
+      const double expn = exp_lib(0.5 * x * x);
       const double ev = x * expn - f0, grad = (1 + x * x) * expn;
       x -= (grad > kEps) ? ev / grad : 0.0;
     }
@@ -1458,7 +1477,7 @@ struct He
     double rough[3] = {0.0, 0.0, 0.0}, weight = 0.0;
     if (APPROX >= 0 && gmin > double(APPROX))
     {
-      for (int c = 0; c < 3; ++c) rough[c] = exp_d(-eb[c] / g[c]) / g[c];
+      for (int c = 0; c < 3; ++c) rough[c] = exp_lib(-eb[c] / g[c]) / g[c];
       weight = fmin(fmax(gmin - double(APPROX), 0.0), 1.0);
     }
     double sum[3] = {0.0, 0.0, 0.0}, gm[3] = {1.0, 1.0, 1.0}, term[3] = {0.0, 0.0, 0.0}, last[3];
@@ -1470,7 +1489,7 @@ struct He
       {
         last[c] = term[c];
         gm[c] *= g[c] / m;
-        term[c] = exp_d(-g[c] - eb[c] / m) * gm[c] / m;
+        term[c] = exp_lib(-g[c] - eb[c] / m) * gm[c] / m;
         sum[c] += term[c];
       }
       if (ADAPTIVE)
