@@ -1135,25 +1135,27 @@ struct Bagher
       // theta > theta0 <=> 2 asin(c) > theta0 <=> c > sin(theta0 / 2) for the half chord c of theta_of (asin is
       // increasing; both sides round, so only lanes within an ulp of the boundary can decide differently, where
       // G1 = 1 + Lambda (1 - e^(c 0^k)) = 1 on either side)
-      hc0[j] = (theta0[j] <= 0.0) ? -1.0 : ((theta0[j] >= kPi) ? 2.0 : sin(0.5 * theta0[j]));
+      // compared as squared chords (4 hc^2 against the chord's squared length: no square root per pair)
+      const double hc = (theta0[j] <= 0.0) ? -1.0 : ((theta0[j] >= kPi) ? 2.0 : sin(0.5 * theta0[j]));
+      hc0[j] = (hc < 0.0) ? -1.0 : 4.0 * hc * hc;
     }
     hc_min = fmin(fmin(hc0[0], hc0[1]), hc0[2]);
     ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
     ggx.iau = ggx.iav = 1.0 / ggx.au;
   }
-  // sgd.h:185-190 G1 for an upper-hemisphere direction with half chord hc (theta = 2 asin(hc)): the branch skips the shadowing
-  // term (a log and two exponentials) where theta <= theta0; th is theta_of(v), evaluated only if some channel
-  // needs it
+  // sgd.h:185-190 G1 for an upper-hemisphere direction with squared chord hc (theta = 2 asin(sqrt(hc) / 2)): the
+  // branch skips the shadowing term (a log and two exponentials) where theta <= theta0; th is theta_of(v),
+  // evaluated only if some channel needs it
   __device__ __forceinline__ double G1h(int j, double hc, double th) const
   {
     double g = 1.0;
     if (hc > hc0[j]) g = 1.0 + Lambda[j] * (1.0 - exp_d(c[j] * pow_d(th - theta0[j], k[j])));
     return g;
   }
-  __device__ __forceinline__ static double half_chord(d3 v)
+  __device__ __forceinline__ static double half_chord(d3 v)     // the squared chord |v - (0, 0, 1)|^2
   {
     const double dz = v.z - 1.0;
-    return 0.5 * sqrt(((0.0 + v.x * v.x) + v.y * v.y) + dz * dz);
+    return ((0.0 + v.x * v.x) + v.y * v.y) + dz * dz;
   }
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {

@@ -264,11 +264,31 @@ struct He
 
   // series length key of the two-phase kernel: lanes with a similar peak position g run similar numbers of terms
   // (0: no series -- the rough approximation alone)
+  // Westin: the terms carry e^(-eb/m), which moves the series' mass to m* ~ the maximum of the log-term
+  // -eb/m + m ln g - ln m!, i.e. eb / m^2 = ln(m / g) (Stirling); the key is m* of the blue channel (the largest g
+  // and eb) by three Newton steps in u = ln m from m = sqrt(eb).  Modelled on 1 M hemisphere pairs (tools/he_geb.py,
+  // the series lengths read back from the GPU): wave-max terms 31.1 with the g key, 27.9 with this one (the true
+  // lengths as key: 23.9).  Only the order of the jobs depends on the key.
   __device__ __forceinline__ int D_key(const DPrep& d) const
   {
     const double g1 = double(d.gg[1]) * double(d.gg[1]);
     const double gmin = fmin(fmin(double(d.gg[0]) * double(d.gg[0]), g1), double(d.gg[2]) * double(d.gg[2]));
     if ((APPROX >= 0) && (gmin - 1.0 > double(APPROX))) return 0;
+#ifndef BBM_HIP_HE_WESTIN_GKEY
+    if (WESTIN)
+    {
+      const float gb = d.gg[2] * d.gg[2], e = d.eb[2];
+      const float lg = __logf(fmaxf(gb, 1e-30f));
+      float u = fmaxf(0.5f * __logf(fmaxf(e, 1.0f)), __logf(fmaxf(gb, 1.0f)));
+#pragma unroll
+      for (int it = 0; it < 3; ++it)
+      {
+        const float ex = e * __expf(-2.0f * u);
+        u -= (ex - u + lg) / (-2.0f * ex - 1.0f);
+      }
+      return 1 + min(30, int(__expf(fminf(fmaxf(u, 0.0f), 4.1588830f))));   // m* in [1, 64]
+    }
+#endif
     return 1 + min(30, int(float(g1) * 1.5f));
   }
 

@@ -35,6 +35,7 @@ struct Bagher
   static constexpr int kParams = 30;
   static constexpr uint32_t kComponent = kFlagSpecular;
   float albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3];
+  float qc0[3], qc_min;   // conservative squared-chord thresholds of theta > theta0 (see G1 below)
   GGX<false> ggx;   // sampling / pdf lobe (ndf/sgd.h:73-93)
 
   __device__ static float avg_alpha(const float* a) { return div_nr(((0.0f + a[0]) + a[1]) + a[2], 3.0f); }
@@ -45,8 +46,18 @@ struct Bagher
     {
       albedo[j] = q[j]; K[j] = q[3 + j]; Lambda[j] = q[6 + j]; c[j] = q[9 + j]; theta0[j] = q[12 + j];
       k[j] = q[15 + j]; alpha[j] = q[18 + j]; p[j] = q[21 + j]; F0[j] = q[24 + j]; F1[j] = q[27 + j];
+      // theta = 2 asin(|v - (0, 0, 1)| / 2) > theta0 needs |v - (0, 0, 1)|^2 > 4 sin^2(theta0 / 2); the threshold is
+      // lowered by 2^-10 relative, far beyond every rounding of either side, so a lane below it has theta <= theta0
+      const float sh = sinf(0.5f * theta0[j]);
+      qc0[j] = (theta0[j] <= 0.0f) ? -1.0f : ((theta0[j] >= kPiF) ? 5.0f : 4.0f * sh * sh * (1.0f - 0x1p-10f));
     }
+    qc_min = fminf(fminf(qc0[0], qc0[1]), qc0[2]);
     ggx.au = ggx.av = avg_alpha(alpha);
+  }
+  __device__ __forceinline__ static float chord2(v3 v)       // |v - (0, 0, 1)|^2 for z(v) >= 0
+  {
+    const float dz = v.z - 1.0f;
+    return ((0.0f + v.x * v.x) + v.y * v.y) + dz * dz;
   }
 
   // ndf::sgd::G1 per channel (ndf/sgd.h:157-193), for a direction with theta(v) = th
@@ -58,6 +69,15 @@ struct Bagher
     // the result is used, and the fit bounds keep k > 0)
     const float g = 1.0f + Lambda[j] * (1.0f - expf_acc(c[j] * powf_xlog(th - theta0[j], k[j])));
     return (th > theta0[j]) ? g : 1.0f;
+  }
+  // the same for an upper-hemisphere direction with squared chord q: lanes below the conservative threshold have
+  // theta <= theta0 and G1 = 1; the others evaluate G1 exactly as above, on a branch (the shadowing term's double
+  // pow and exp are skipped where no lane of the wave needs them -- at the default theta0 = pi/2, every lane)
+  __device__ __forceinline__ float G1q(int j, float q, float th) const
+  {
+    float g = 1.0f;
+    if (q > qc0[j]) g = G1(j, th);
+    return g;
   }
 
   template<int MODE>
@@ -74,7 +94,11 @@ struct Bagher
       const double dnorm = double(kPiF) * (z2 * z2);      // Constants::Pi() * pow(cos, 4.0) (sgd.h:62)
       // uncorrelated (uncorrelated.h:30-42) + sgd::G1 masks: z(v) > 0 and v.m > 0 for both
       const bool gmask = (inh > 0) && (outh > 0);
-      const float th_in = theta_of(in), th_out = theta_of(out);
+      // in.z, out.z > 0 on every lane whose result is used: theta_of only where a channel may need it
+      const float q_in = chord2(in), q_out = chord2(out);
+      float th_in = 0.0f, th_out = 0.0f;
+      if (q_in > qc_min) th_in = theta_of(in);
+      if (q_out > qc_min) th_out = theta_of(out);
       const float cosF = 0.5f * (inh + outh);
       const double x = double(1.0f - cosF);
       const double x5 = (x * x) * (x * x) * x;
@@ -89,7 +113,7 @@ struct Bagher
         const float den = powf_fast(t, p[j]);
         const float P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
         const float Dj = ((h.z > 0) ? f_div_d(double(P22), dnorm) : 0.0f) * K[j];
-        const float Gj = gmask ? G1(j, th_in) * G1(j, th_out) : 0.0f;
+        const float Gj = gmask ? G1q(j, q_in, th_in) * G1q(j, q_out, th_out) : 0.0f;
         // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
         const float S = float(double(F0[j]) + double(1.0f - F0[j]) * x5);
         const float Fj = S - F1[j] * cosF;
