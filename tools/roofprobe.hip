@@ -140,6 +140,70 @@ __global__ __launch_bounds__(256) void k_probe_chunk(Args a)
   }
 }
 
+// variants 12-14: the reference's own pair layout -- a Vec3dPair array (in xyz, out xyz: 24 B per pair, one
+// stream) in, (r, g, b, pdf) float4 per pair (one stream) out; nontemporal.  a.in[0] / a.out[0] are the two
+// arrays, n4 counts quads of pairs.
+//   12: one pair per lane, lane-consecutive pairs (two 12 B loads, one 16 B store per lane)
+//   13: four consecutive pairs per lane (six 16 B loads, four 16 B stores: lanes 96 B / 64 B apart)
+//   14: four pairs per lane at wave stride 64 (pairs w*256 + k*64 + lane), 8 loads of 12 B in flight
+struct P3 { float x, y, z; };
+template<int V>
+__global__ __launch_bounds__(256) void k_probe_aos(Args a)
+{
+  const float* in = reinterpret_cast<const float*>(a.in[0]);
+  f4* out = a.out[0];
+  const uint64_t npairs = a.n4 * 4;
+  if (V == 12)
+  {
+    for (uint64_t p = uint64_t(blockIdx.x) * 256 + threadIdx.x; p < npairs; p += uint64_t(gridDim.x) * 256)
+    {
+      const float* q = in + p * 6;
+      const float ix = __builtin_nontemporal_load(q + 0), iy = __builtin_nontemporal_load(q + 1), iz = __builtin_nontemporal_load(q + 2);
+      const float ox = __builtin_nontemporal_load(q + 3), oy = __builtin_nontemporal_load(q + 4), oz = __builtin_nontemporal_load(q + 5);
+      __builtin_nontemporal_store(f4{ix + ox, iy + oy, iz + oz, ix * oz}, &out[p]);
+    }
+    return;
+  }
+  if (V == 13)
+  {
+    const f4* in4 = a.in[0];
+    for (uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x; t < a.n4; t += uint64_t(gridDim.x) * 256)
+    {
+      f4 v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = __builtin_nontemporal_load(&in4[t * 6 + k]);
+      __builtin_nontemporal_store(f4{v[0].x + v[0].w, v[0].y + v[1].x, v[0].z + v[1].y, v[0].x * v[1].z}, &out[t * 4 + 0]);
+      __builtin_nontemporal_store(f4{v[1].w + v[2].z, v[2].x + v[2].w, v[2].y + v[3].x, v[1].w * v[3].x}, &out[t * 4 + 1]);
+      __builtin_nontemporal_store(f4{v[3].y + v[4].y, v[3].z + v[4].z, v[3].w + v[4].w, v[3].y * v[4].w}, &out[t * 4 + 2]);
+      __builtin_nontemporal_store(f4{v[5].x + v[5].w, v[5].y + v[5].x, v[5].z + v[5].y, v[5].x * v[5].z}, &out[t * 4 + 3]);
+    }
+    return;
+  }
+  if (V == 14)
+  {
+    const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t base = (uint64_t(blockIdx.x) * 4 + wave) * 256; base < npairs; base += uint64_t(gridDim.x) * 1024)
+    {
+      float v[4][6];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+      {
+        const uint64_t p = base + k * 64 + lane;
+        const float* q = in + (p < npairs ? p : npairs - 1) * 6;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) v[k][c] = __builtin_nontemporal_load(q + c);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+      {
+        const uint64_t p = base + k * 64 + lane;
+        if (p < npairs) __builtin_nontemporal_store(f4{v[k][0] + v[k][3], v[k][1] + v[k][4], v[k][2] + v[k][5], v[k][0] * v[k][5]}, &out[p]);
+      }
+    }
+    return;
+  }
+}
+
 extern "C" int roofprobe(int variant, const float* const* in, float* const* out, uint64_t n, int blocks, void* stream)
 {
   Args a;
@@ -161,6 +225,9 @@ extern "C" int roofprobe(int variant, const float* const* in, float* const* out,
     case 9: hipLaunchKernelGGL(k_probe_chunk<16>, dim3((a.n4 + 16 * 256 - 1) / (16 * 256)), dim3(256), 0, s, a); break;
     case 10: hipLaunchKernelGGL(k_probe_chunk<64>, dim3((a.n4 + 64 * 256 - 1) / (64 * 256)), dim3(256), 0, s, a); break;
     case 11: hipLaunchKernelGGL(k_probe_chunk<4>, dim3((a.n4 + 4 * 256 - 1) / (4 * 256)), dim3(256), 0, s, a); break;
+    case 12: hipLaunchKernelGGL(k_probe_aos<12>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 13: hipLaunchKernelGGL(k_probe_aos<13>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 14: hipLaunchKernelGGL(k_probe_aos<14>, dim3(blocks), dim3(256), 0, s, a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
