@@ -27,6 +27,7 @@ _SZ = ctypes.c_size_t
 
 SIGNATURES = {
     "bbm_hip_abi_version": (_I, []),
+    "bbm_hip_set_exact_subnormals": (_I, [_I]),
     "bbm_hip_last_error": (ctypes.c_char_p, []),
     "bbm_hip_num_models": (_I, []),
     "bbm_hip_model_name": (ctypes.c_char_p, [_I]),
@@ -71,7 +72,7 @@ SIGNATURES = {
     "bbm_hip_scratch_bytes": (_SZ, []),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
 
 

@@ -651,6 +651,15 @@ def scratch_bytes():
     return int(_lib.load().bbm_hip_scratch_bytes())
 
 
+def set_exact_subnormals(on):
+    """Exact-subnormal mode of the Beckmann microfacet models' eval / pdf kernels (bbm_hip_set_exact_subnormals,
+    process-wide): on, the quotients a subnormal intermediate can reach round on the subnormal grid as the
+    reference's IEEE divisions do, and CookTorrance & co. return the reference's floats bit for bit (+4.3 % kernel
+    time on the headline); off (default), outputs below ~2e-34 may differ in the last bit.  Returns the previous
+    setting."""
+    return bool(_lib.load().bbm_hip_set_exact_subnormals(1 if on else 0))
+
+
 def fill_directions(seed, stream_id, offset, n, mode=0, out=None, stream=None):
     """Counter-based synthetic directions (bbm_hip_fill_directions) -> (3, n) float32 CUDA tensor."""
     torch = _torch()

@@ -529,6 +529,8 @@ extern "C" {
 
 int bbm_hip_abi_version(void) { return BBM_HIP_ABI_VERSION; }
 
+int bbm_hip_set_exact_subnormals(int on) { return exact_subnormals().exchange(on != 0 ? 1 : 0); }
+
 size_t bbm_hip_scratch_trim(void) { return scratch_trim(); }
 
 size_t bbm_hip_scratch_bytes(void) { return scratch_bytes(); }

@@ -1182,7 +1182,12 @@ struct Bagher
     {
       const double t = alpha[j] + tan2 * inv_alpha[j];
       const double lden = p[j] * log2_d(t);
+#ifdef BBM_HIP_F64_BAGHER_EXPD
       const double P22 = (lden > -52.0) ? exp_d(-__builtin_fma(lden, 0x1.62e42fefa39efp-1, t)) : 0.0;
+#else
+      // a factor of D, not cancelled: exp_dd's ~2^-44 (9 FMAs) instead of exp_d's full double (15 FMAs)
+      const double P22 = (lden > -52.0) ? exp_dd(fmax(-__builtin_fma(lden, 0x1.62e42fefa39efp-1, t), -1.0e4)) : 0.0;
+#endif
       const double Dj = ((h.z > 0) ? P22 * inv_dnorm : 0.0) * K[j];
       const double Gj = gmask ? G1h(j, hc_in, th_in) * G1h(j, hc_out, th_out) : 0.0;
       const double Fj = (F0[j] + (1.0 - F0[j]) * x5) - F1[j] * cosF;

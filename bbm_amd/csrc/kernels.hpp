@@ -12,6 +12,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -68,13 +69,38 @@ struct EvalArgs
   ParamBlock p;
 };
 
-template<class Model, int MODE>
+// Models with an exact-subnormal evaluation (Microfacet over Beckmann: Model::kHasExact, microfacet.hpp) get a
+// second instantiation of the eval kernels, launched when bbm_hip_set_exact_subnormals is on.
+template<class Model> constexpr bool model_has_exact()
+{
+  if constexpr (requires { Model::kHasExact; }) return Model::kHasExact;
+  else return false;
+}
+template<int MODE, bool EXACT, class Model>
+__device__ __forceinline__ void model_eval_pdf(const Model& m, v3 in, v3 out, uint32_t comp, float* rgb, float& pdf)
+{
+  if constexpr (EXACT) m.template eval_pdf<MODE, true>(in, out, comp, rgb, pdf);
+  else m.template eval_pdf<MODE>(in, out, comp, rgb, pdf);
+}
+// process-wide switch (bbm_hip_set_exact_subnormals; initial value from BBM_HIP_EXACT_SUBNORMALS)
+inline std::atomic<int>& exact_subnormals()
+{
+  static std::atomic<int> v{[] {
+    const char* e = std::getenv("BBM_HIP_EXACT_SUBNORMALS");
+    return (e && std::atoi(e) != 0) ? 1 : 0;
+  }()};
+  return v;
+}
+
+template<class Model> inline bool exact_launch() { return model_has_exact<Model>() && exact_subnormals().load() != 0; }
+
+template<class Model, int MODE, bool EXACT = false>
 __device__ __forceinline__ void one_pair(const Model& m, const EvalArgs& a, uint64_t i, bool active)
 {
   float rgb[3], pdf;
   const v3 in = mk3(a.ix[i], a.iy[i], a.iz[i]);
   const v3 out = mk3(a.ox[i], a.oy[i], a.oz[i]);
-  m.template eval_pdf<MODE>(in, out, active ? a.component : 0u, rgb, pdf);
+  model_eval_pdf<MODE, EXACT>(m, in, out, active ? a.component : 0u, rgb, pdf);
   if (MODE & kModeEval) { a.r[i] = rgb[0]; a.g[i] = rgb[1]; a.b[i] = rgb[2]; }
   if (MODE & kModePdf) a.pdf[i] = pdf;
 }
@@ -119,7 +145,7 @@ template<class Model> struct eval_waves { static constexpr int value = 1; };
 // per thread) a capped grid-stride launch amortises it over several iterations.
 template<class Model> struct eval_grid_cap { static constexpr uint64_t value = 0; };
 
-template<class Model, int MODE, bool MASK, bool NT>
+template<class Model, int MODE, bool MASK, bool NT, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_waves_per_eu(eval_waves<Model>::value, 8)))
 void k_eval_pdf_v4(EvalArgs a)
 {
@@ -144,7 +170,7 @@ void k_eval_pdf_v4(EvalArgs a)
     {
       float rgb[3];
       const uint32_t comp = ((mk >> (8 * j)) & 0xffu) ? a.component : 0u;
-      m.template eval_pdf<MODE>(mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
+      model_eval_pdf<MODE, EXACT>(m, mk3(inx[j], iny[j], inz[j]), mk3(onx[j], ony[j], onz[j]), comp, rgb, p[j]);
       r[j] = rgb[0]; g[j] = rgb[1]; b[j] = rgb[2];
     }
     if (MODE & kModeEval)
@@ -159,7 +185,7 @@ void k_eval_pdf_v4(EvalArgs a)
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))
   {
     const uint64_t i = (n4 << 2) + threadIdx.x;
-    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+    one_pair<Model, MODE, EXACT>(m, a, i, MASK ? (a.mask[i] != 0) : true);
   }
 }
 
@@ -279,13 +305,13 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_pipe(EvalArgs a)
 }
 
 // Scalar path for unaligned arrays.
-template<class Model, int MODE, bool MASK>
+template<class Model, int MODE, bool MASK, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
 {
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
-    one_pair<Model, MODE>(m, a, i, MASK ? (a.mask[i] != 0) : true);
+    one_pair<Model, MODE, EXACT>(m, a, i, MASK ? (a.mask[i] != 0) : true);
 }
 
 // Models whose per-pair eval is VALU-heavy AND returns exactly zero (rgb and pdf) for every pair outside the
@@ -640,6 +666,14 @@ int launch_mode(const EvalArgs& a0, hipStream_t s)
 #endif
   if (vec && compact_eval<Model>::value && use_compact())
     hipLaunchKernelGGL((k_eval_pdf_compact<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  else if (exact_launch<Model>())
+  {
+    if constexpr (model_has_exact<Model>())
+    {
+      if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+    }
+  }
   else if (vec) hipLaunchKernelGGL((k_eval_pdf_v4<Model, MODE, MASK, true>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_eval_pdf_v1<Model, MODE, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();

@@ -88,6 +88,27 @@ __device__ __forceinline__ float div_nr(float n, float d)
 #endif
 }
 
+// n / d correctly rounded on the subnormal grid as well (EXACT), for a finite normal d and any float n: the f32
+// reciprocal seed q = n rcp(d) (~2^-22 relative), one remainder step in double (n - d q is exact in double: a 48-bit
+// product and a cancelling difference), rounded once to float -- the IEEE float quotient except within ~2^-22 ulp of
+// a rounding midpoint, subnormal numerators and quotients included, where div_nr's f32 remainder is itself rounded
+// to the subnormal grid.  For the sites where a subnormal intermediate can flow into a normal output (the Beckmann D
+// of a far-tail halfway vector and the two quotients downstream of it); EXACT = false is div_nr.  Selected per
+// launch (bbm_hip_set_exact_subnormals): measured +4.3 % on the headline kernel (0.703 -> 0.734 ms per 100 M pairs),
+// CookTorrance eval+pdf then bit-identical to the reference on every lane of the 1 M-pair batches.  d = 0 / inf /
+// NaN give inf / NaN, which those sites select away.
+template<bool EXACT>
+__device__ __forceinline__ float div_sub(float n, float d)
+{
+  if constexpr (EXACT)
+  {
+    const float r = __builtin_amdgcn_rcpf(d);
+    const double q0 = double(n * r);
+    return float(__builtin_fma(__builtin_fma(-double(d), q0, double(n)), double(r), q0));
+  }
+  else return div_nr(n, d);
+}
+
 // a / d for the quotients that are a normal float or exactly 0 on every lane whose result is used (a finite
 // nonzero divisor bounded away from the subnormal range, e.g. 1 / |h| with |h|^2 in (0, 4], or Fresnel's
 // (g - c) / (g + c) with c > 0): the Markstein step alone, no special-case select.  Same result as div_nr there.
@@ -207,6 +228,22 @@ __device__ __constant__ const uint64_t kExpfTab[32] = {
     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+// kExpfTab[j] for a per-lane j in [0, 32).  Default: a 64-bit gather from the constant table (an L1/L2 hit, but
+// a dependent memory access queued behind the kernel's streaming loads).  -DBBM_HIP_EXPF_BPERM: every lane holds
+// entry (lane & 31) in two VGPRs (one load per wave, loop-invariant) and the lookup is two ds_bpermute_b32 --
+// cross-lane moves through the LDS crossbar, no memory access.
+__device__ __forceinline__ uint64_t expf_tab(uint32_t j)
+{
+#ifdef BBM_HIP_EXPF_BPERM
+  const uint64_t mine = kExpfTab[__lane_id() & 31u];
+  const int lo = __builtin_amdgcn_ds_bpermute(int(j << 2), int(uint32_t(mine)));
+  const int hi = __builtin_amdgcn_ds_bpermute(int(j << 2), int(uint32_t(mine >> 32)));
+  return (uint64_t(uint32_t(hi)) << 32) | uint32_t(lo);
+#else
+  return kExpfTab[j];
+#endif
+}
+
 __device__ __forceinline__ float expf_glibc(float x)
 {
   constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
@@ -222,7 +259,7 @@ __device__ __forceinline__ float expf_glibc(float x)
   // timing probe only (tools/build_variant.sh): the table gather replaced by arithmetic of the same shape (wrong values)
   const double s = __builtin_bit_cast(double, (0x3fef000000000000ull | ((ki & 31u) << 40)) + (ki << 47));
 #else
-  const double s = __builtin_bit_cast(double, kExpfTab[ki & 31u] + (ki << 47));   // 2^(k/N)
+  const double s = __builtin_bit_cast(double, expf_tab(ki & 31u) + (ki << 47));   // 2^(k/N)
 #endif
   const double z = __builtin_fma(kC0, r, kC1);
   const double r2 = r * r;
@@ -257,7 +294,7 @@ __device__ __forceinline__ float expf_glibc_neg(float x)
   const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
   const double kd = kb - kShift;
   const double r = __builtin_fma(kInvLn2N, xd, -kd);
-  const double s = __builtin_bit_cast(double, kExpfTab[ki & 31u] + (ki << 47));
+  const double s = __builtin_bit_cast(double, expf_tab(ki & 31u) + (ki << 47));
   const double z = __builtin_fma(kC0, r, kC1);
   const double r2 = r * r;
   double y = __builtin_fma(kC2, r, 1.0);
@@ -414,6 +451,22 @@ __device__ __forceinline__ float div_ff(float nh, float nl, float dh, float dl)
 #else
   return __builtin_isnormal(q1) ? q1 : nh * r;     // subnormal / special results: see div_nr
 #endif
+}
+
+// nh / (dh + dl) as div_sub: the f32 seed and one remainder step in double (dh + dl exact in double), rounded
+// once -- for a subnormal numerator too (the Cook-normalised eval of a far-tail halfway vector); EXACT = false is
+// div_ff
+template<bool EXACT>
+__device__ __forceinline__ float div_ff_sub(float nh, float dh, float dl)
+{
+  if constexpr (EXACT)
+  {
+    const float r = __builtin_amdgcn_rcpf(dh);
+    const double q0 = double(nh * r);
+    const double dd = double(dh) + double(dl);
+    return float(__builtin_fma(__builtin_fma(-dd, q0, double(nh)), double(r), q0));
+  }
+  else return div_ff(nh, 0.0f, dh, dl);
 }
 
 // horizontal.h:78-82: dot = inner_product(a, b, T(0)) -> ((0 + a0 b0) + a1 b1) + a2 b2

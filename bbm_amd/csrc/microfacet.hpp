@@ -33,7 +33,9 @@ struct Beckmann
   float au, av;
   __device__ explicit Beckmann(const float* p) : au(p[0]), av(Aniso ? p[1] : p[0]) {}
 
-  // beckmann.h:49-66: exp(-|h.xy/alpha|^2 / cos^2) / (au av cos^4) [x 1/pi if Normalize]
+  // beckmann.h:49-66: exp(-|h.xy/alpha|^2 / cos^2) / (au av cos^4) [x 1/pi if Normalize]; EXACT: the quotient
+  // correctly rounded on the subnormal grid too (div_sub)
+  template<bool EXACT = false>
   __device__ __forceinline__ float eval(v3 h) const
   {
     const float c2 = h.z * h.z;
@@ -43,7 +45,7 @@ struct Beckmann
 #elif defined(BBM_HIP_BECKMANN_EXP_RN)
     float D = div_nr(expf_rn(div_nr(-sn, c2)), au * av * c2 * c2);      // A/B: correctly rounded
 #else
-    float D = div_nr(expf_glibc_neg(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit (x <= 0)
+    float D = div_sub<EXACT>(expf_glibc_neg(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit (x <= 0)
 #endif
     if (Normalize) D *= kInvPiF;
     return (h.z > 0) ? D : 0.0f;
@@ -442,7 +444,7 @@ enum : int { kModeEval = 1, kModePdf = 2, kModeEvalPdf = 3 };
 constexpr float kPiHi = 3.14159274101257324f;    // RN_f(pi)
 constexpr float kPiLo = -8.74227766e-08f;        // RN_f(pi - kPiHi)
 
-template<Norm N>
+template<Norm N, bool EXACT = false>
 __device__ __forceinline__ float eval_scale(float x, float y)
 {
   if (N == Norm::Cook)
@@ -450,10 +452,10 @@ __device__ __forceinline__ float eval_scale(float x, float y)
     float dh, dl;
     two_prod(y, kPiHi, dh, dl);
     dl = __builtin_fmaf(y, kPiLo, dl);
-    return div_ff(x, 0.0f, dh, dl);
+    return div_ff_sub<EXACT>(x, dh, dl);
   }
   // Walter: (x / 4.0) / y in double = x / (4 y), 4 y exact in float (x * 0.25f would round a subnormal x)
-  return div_nr(x, N == Norm::Walter ? 4.0f * y : y);
+  return div_sub<EXACT>(x, N == Norm::Walter ? 4.0f * y : y);
 }
 
 template<class NDF, class MS, class FRESNEL, Norm N, bool Scaled>
@@ -473,8 +475,12 @@ struct Microfacet
     albedo[2] = Scaled ? p[2] : 1.0f;
   }
 
+  // EXACT (bbm_hip_set_exact_subnormals): the quotients a subnormal intermediate can reach rounded on the subnormal
+  // grid as the reference's IEEE divisions are (div_sub) -- for NDFs with such an evaluation (Beckmann)
+  static constexpr bool kHasExact = requires(const NDF& d, v3 v) { d.template eval<true>(v); };
+
   // microfacet.h:74-102 (eval) + :154-174 (pdf), fused: both share the halfway vector and D(h).
-  template<int MODE>
+  template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     // Branch-free: every term is computed and the masks are applied with selects, so the four
@@ -485,7 +491,9 @@ struct Microfacet
     const v3 h = halfway(in, out);
     // pdf's `h = z(h) < 0 ? -h : h` (:167) never fires on active lanes: z(in + out) > 0 and
     // normalize scales by a positive factor, so h is used as is.
-    const float D = ndf.eval(h);
+    float D;
+    if constexpr (EXACT && kHasExact) D = ndf.template eval<true>(h);
+    else D = ndf.eval(h);
     const float outh = dot3(out, h);
     if (MODE & kModeEval)
     {
@@ -493,7 +501,7 @@ struct Microfacet
       const float G = MS::eval(ndf, in, out, h, inh, outh);
       const float F = fresnel.eval(0.5f * (inh + outh));
       // (D G F) / NormalizationFactor / (z_in z_out): literal<double> promotes to double
-      const float res = eval_scale<N>(D * G * F, in.z * out.z);
+      const float res = eval_scale<N, EXACT && kHasExact>(D * G * F, in.z * out.z);
       rgb[0] = active ? (Scaled ? res * albedo[0] : res) : 0.0f;
       rgb[1] = active ? (Scaled ? res * albedo[1] : res) : 0.0f;
       rgb[2] = active ? (Scaled ? res * albedo[2] : res) : 0.0f;
@@ -502,7 +510,7 @@ struct Microfacet
     if (MODE & kModePdf)
     {
       // float(p / (4.0 * |o.h|)): float operands, one double op -> identical to the float division
-      const float p = div_nr(ndf.pdf(out, h, D), 4.0f * fabsf(outh));
+      const float p = div_sub<EXACT && kHasExact>(ndf.pdf(out, h, D), 4.0f * fabsf(outh));
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;

@@ -73,7 +73,8 @@ def parse(argv=None):
                          "(a ~0.2 ms kernel, e.g. 12.5M pairs per GPU under --scaling strong on 8 GPUs). Both figures "
                          "are reported; value is the graph-timed one when the graph is used")
     ap.add_argument("--graph-below", type=int, default=30_000_000)
-    ap.add_argument("--fit-max-steps", type=int, default=3000, help="fit: compass steps cap for the convergence run")
+    ap.add_argument("--fit-max-steps", type=int, default=200000, help="fit: compass steps cap for the convergence run")
+    ap.add_argument("--fit-max-seconds", type=float, default=120.0, help="fit: wall-time cap for the convergence run")
     ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "f64", "selftest"],
                     help="evalpdf: the BASELINE metric (config 2, default); models: every model's eval over shared "
                          "pairs (config 3); sample: importance-sample -> eval -> pdf MC loop (config 4); fit: "

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 8
+#define BBM_HIP_ABI_VERSION 9
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -57,6 +57,15 @@ int bbm_hip_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
 const char* bbm_hip_last_error(void);
+
+/* Exact-subnormal mode (process-wide, default off; initial value from the environment variable
+ * BBM_HIP_EXACT_SUBNORMALS).  On: the eval / pdf kernels of the Beckmann microfacet models (CookTorrance and its
+ * Walter / Heitz / Ngan variants) take the three quotients a subnormal intermediate can reach (D, the Cook
+ * normalisation, the pdf's 1 / (4 |o.h|)) with a double remainder step, so eval and pdf are the reference's floats
+ * bit for bit on every lane (ndf/beckmann.h:60 -> glibc expf, microfacet.h:100, :171), at +4.3 % kernel time on
+ * the headline.  Off: those quotients use the f32 remainder step; outputs below ~2e-34 may differ in the last
+ * bit (the per-lane parity bar holds either way).  Returns the previous setting (0 / 1), or a negative code. */
+int bbm_hip_set_exact_subnormals(int on);
 
 /* Model registry.  Replaces the compile-time registry of BBM_EXPORT_BSDFMODEL
  * (e.g. include/bsdfmodel/cooktorrance.h:42) and the keyword lookup of

@@ -258,6 +258,49 @@ def test_large_batch_vs_reference(bbm, mode_in, mode_out):
     _report(f"large_{mode_in}{mode_out}", stats)
 
 
+EXACT_MODELS = ("CookTorrance", "CookTorranceWalter", "CookTorranceHeitz", "NganCookTorrance")
+
+
+@pytest.mark.parametrize("mode_in,mode_out", [(0, 1), (0, 0)])
+def test_exact_subnormal_mode_is_bit_exact(bbm, mode_in, mode_out):
+    """bbm_hip_set_exact_subnormals(1): the Beckmann microfacet models' eval + pdf equal the reference's floats on
+    every lane of 1M pairs per parameter set (the quotients reached by subnormal intermediates rounded as glibc's
+    IEEE divisions; bit-exact fraction >= 0.9999), and differ from the default mode only on values below 1e-30.
+    Unaligned sizes take the scalar kernel's exact instantiation."""
+    n = 1 << 20
+    din = bbm.fill_directions(0xBB5EED, 0, 0, n, mode=mode_in).cpu().numpy()
+    dout = bbm.fill_directions(0xBB5EED, 1, 0, n, mode=mode_out).cpu().numpy()
+    stats = {}
+    try:
+        for name in EXACT_MODELS:
+            g = ou.golden_model(name)
+            for si in range(len(META["models"][name]["sets"])):
+                params = g[f"params{si}"]
+                m = bbm.BsdfModel(name)
+                m.set_parameter_values(params)
+                assert bbm.set_exact_subnormals(False) in (False, True)
+                fast = _gpu_evalpdf(m, din, dout)
+                assert bbm.set_exact_subnormals(True) is False
+                got = _gpu_evalpdf(m, din, dout)
+                # scalar kernel: row views starting one float in (4 B-aligned pointers)
+                di, do = torch.from_numpy(din).cuda(), torch.from_numpy(dout).cuda()
+                o_rgb, o_pdf = m.eval_pdf(tuple(di[i, 1:n - 2] for i in range(3)), tuple(do[i, 1:n - 2] for i in range(3)))
+                odd = torch.cat([o_rgb, o_pdf[None]]).cpu().numpy()
+                ref = ou.oracle_eval_pdf(name, params, din, dout, nthreads=8)
+                s = check_lanes(got, ref, f"exact {name}[{si}] {mode_in}{mode_out}",
+                                _evalpdf_provers(bbm, name, params, din, dout, got))
+                assert s["frac_bit_exact"] >= 0.9999, f"exact {name}[{si}]: {s}"
+                assert np.array_equal(odd, got[:, 1:n - 2], equal_nan=True), f"exact {name}[{si}]: scalar kernel differs"
+                diff = ~((fast == got) | (np.isnan(fast) & np.isnan(got)))
+                s["max_ref_where_modes_differ"] = float(np.abs(ref[diff]).max()) if diff.any() else 0.0
+                assert s["max_ref_where_modes_differ"] < 1e-30, f"exact {name}[{si}]: modes differ above 1e-30 ({s})"
+                s["frac_bit_exact_default_mode"] = float(np.mean(ou.ulp_diff(fast, ref) == 0))
+                stats[f"{name}[{si}]"] = s
+    finally:
+        bbm.set_exact_subnormals(False)
+    _report(f"exact_{mode_in}{mode_out}", stats)
+
+
 def test_mask_lanes_are_zero_and_others_untouched(bbm):
     n = 4099
     din = bbm.fill_directions(3, 0, 0, n, mode=0)

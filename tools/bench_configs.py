@@ -227,7 +227,8 @@ def bench_fit(args, dist, rank, world):
     MERL bin centres into a MERL-format .binary and read back through bbm_amd.Merl, as a real MERL file would be;
     the fitted model is Aggregate(Lambertian, Bagher) at its defaults.  value: probe-pair evaluations/s of a
     compass step's 2P probes (one bbm_hip_loss launch + the RCCL all-reduce), K timed steps; then the compass
-    search runs from the defaults to convergence (compass.h:82-140, step size < eps) or --fit-max-steps, and the
+    search runs from the defaults to convergence (compass.h:82-140, step size < eps) or --fit-max-steps /
+    --fit-max-seconds, and the
     line reports its steps, wall time per step and the loss before / after."""
     name = "Aggregate<Lambertian,Bagher>"
     mat, mstr = fit_material()
@@ -247,7 +248,7 @@ def bench_fit(args, dist, rank, world):
     loss0 = float(comp.loss_value)
     t0 = time.perf_counter()
     steps = 0
-    while not comp.is_converged() and steps < args.fit_max_steps:
+    while not comp.is_converged() and steps < args.fit_max_steps and time.perf_counter() - t0 < args.fit_max_seconds:
         comp.step()
         steps += 1
     torch.cuda.synchronize()
@@ -266,7 +267,8 @@ def bench_fit(args, dist, rank, world):
                "probe_pairs_per_dispatch": len(probes) * (pairs // world),
                "roofline": valu_roofline("fit:Aggregate", kern_ms, len(probes) * (pairs // world)),
                "fit": {"from": "Aggregate<Lambertian,Bagher> defaults", "steps": steps,
-                       "converged": comp.is_converged(), "max_steps": args.fit_max_steps, "seconds": fit_s,
+                       "converged": comp.is_converged(), "max_steps": args.fit_max_steps,
+                       "max_seconds": args.fit_max_seconds, "seconds": fit_s,
                        "ms_per_compass_step": fit_s * 1e3 / max(steps, 1), "loss_start": loss0,
                        "loss_end": float(comp.loss_value), "final_step_size": float(comp.step_size)}})
 
