@@ -654,8 +654,8 @@ def scratch_bytes():
 def set_exact_subnormals(on):
     """Exact-subnormal mode of the Beckmann microfacet models' eval / pdf kernels (bbm_hip_set_exact_subnormals,
     process-wide): on, the quotients a subnormal intermediate can reach round on the subnormal grid as the
-    reference's IEEE divisions do, and CookTorrance & co. return the reference's floats bit for bit (+4.3 % kernel
-    time on the headline); off (default), outputs below ~2e-34 may differ in the last bit.  Returns the previous
+    reference's IEEE divisions do, and CookTorrance & co. return the reference's floats bit for bit (+3.6-4.3 % kernel
+    time on the headline); off (default), outputs below ~1e-30 may differ in the last bit.  Returns the previous
     setting."""
     return bool(_lib.load().bbm_hip_set_exact_subnormals(1 if on else 0))
 

@@ -94,7 +94,7 @@ __device__ __forceinline__ float div_nr(float n, float d)
 // a rounding midpoint, subnormal numerators and quotients included, where div_nr's f32 remainder is itself rounded
 // to the subnormal grid.  For the sites where a subnormal intermediate can flow into a normal output (the Beckmann D
 // of a far-tail halfway vector and the two quotients downstream of it); EXACT = false is div_nr.  Selected per
-// launch (bbm_hip_set_exact_subnormals): measured +4.3 % on the headline kernel (0.703 -> 0.734 ms per 100 M pairs),
+// launch (bbm_hip_set_exact_subnormals): measured +3.6-4.3 % on the headline kernel (0.703 -> 0.734, 0.726 -> 0.752 ms per 100 M pairs),
 // CookTorrance eval+pdf then bit-identical to the reference on every lane of the 1 M-pair batches.  d = 0 / inf /
 // NaN give inf / NaN, which those sites select away.
 template<bool EXACT>

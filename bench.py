@@ -66,6 +66,7 @@ def parse(argv=None):
     ap.add_argument("--models", default=None, help="comma-separated subset of models for --workload models|sample "
                                                    "(counter passes profile one model at a time)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-exact", action="store_true", help="evalpdf: skip the exact-subnormal mode's timing")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="evalpdf: time the K steps as HIP-graph replays of R launches (K/R replays, R | K) instead of "
@@ -196,6 +197,21 @@ def main(argv=None):
                                  "rank_ms_per_step": [t * 1e3 / args.steps for t in g_per]}
         elapsed, kern_ms, per_rank = g_el, g_ms / reps, g_per
 
+    # the same K steps in the exact-subnormal mode (bbm_hip_set_exact_subnormals: every lane the reference's float;
+    # the Beckmann microfacet models only), reported beside the default mode's figure, not as the value
+    exact = None
+    if world == 1 and not args.no_exact:
+        prev = bbm_amd.set_exact_subnormals(True)
+        try:
+            e_el, e_ms, _, _ = bh.timed(launch, argparse.Namespace(**{**vars(args), "warmup": 5, "settle_s": 0.1}),
+                                        dist, stream)
+        finally:
+            bbm_amd.set_exact_subnormals(prev)
+        exact = {"value": n * args.steps / e_el, "kernel_ms": e_ms,
+                 "roofline_frac": BYTES_PER_PAIR_MODEL.get(args.model, BYTES_PER_PAIR) * n / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "note": "bit-identical to the reference on every lane (tests/test_gpu_parity.py::"
+                         "test_exact_subnormal_mode_is_bit_exact); default mode: outputs below ~1e-30 may differ in the last bit"}
+
     # sanity: outputs finite and non-trivial
     ok = bool(torch.isfinite(pdf).all()) and float(rgb[0].abs().max()) > 0
 
@@ -239,6 +255,8 @@ def main(argv=None):
             "outputs_ok": ok,
             "settle": {"seconds": args.settle_s, "extra_untimed_steps": settle},
         }
+        if exact is not None:
+            line["exact_subnormals_mode"] = exact
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(model, din, dout, args.cpu_seconds)
         print(json.dumps(line), flush=True)

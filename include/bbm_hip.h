@@ -62,8 +62,8 @@ const char* bbm_hip_last_error(void);
  * BBM_HIP_EXACT_SUBNORMALS).  On: the eval / pdf kernels of the Beckmann microfacet models (CookTorrance and its
  * Walter / Heitz / Ngan variants) take the three quotients a subnormal intermediate can reach (D, the Cook
  * normalisation, the pdf's 1 / (4 |o.h|)) with a double remainder step, so eval and pdf are the reference's floats
- * bit for bit on every lane (ndf/beckmann.h:60 -> glibc expf, microfacet.h:100, :171), at +4.3 % kernel time on
- * the headline.  Off: those quotients use the f32 remainder step; outputs below ~2e-34 may differ in the last
+ * bit for bit on every lane (ndf/beckmann.h:60 -> glibc expf, microfacet.h:100, :171), at +3.6-4.3 % kernel time on
+ * the headline.  Off: those quotients use the f32 remainder step; outputs below ~1e-30 may differ in the last
  * bit (the per-lane parity bar holds either way).  Returns the previous setting (0 / 1), or a negative code. */
 int bbm_hip_set_exact_subnormals(int on);
 

@@ -8,7 +8,7 @@ mkdir -p gpurun_out/final
 timeout -k 10 300 python bench.py > gpurun_out/final/bench.json 2> gpurun_out/final/bench.err || { echo "bench failed"; tail -20 gpurun_out/final/bench.err; exit 1; }
 cut -c1-300 gpurun_out/final/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu > "$R/gpurun_out/final/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/final/prof.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/final/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu --no-exact > "$R/gpurun_out/final/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/final/prof.log"; exit 1; }
 cd "$R"
 bash tools/gpu_traffic.sh || exit 1
 for W in models sample fit f64; do
