@@ -64,6 +64,15 @@ namespace bbm {
       if(rc < 0) throw error(rc, bbm_hip_last_error());
     }
 
+    //! \brief Exact-subnormal mode (bbm_hip_set_exact_subnormals, process-wide): the Beckmann microfacet models'
+    //!        eval / pdf bit for bit the reference's floats on every lane; returns the previous setting
+    inline bool set_exact_subnormals(bool on)
+    {
+      const int prev = bbm_hip_set_exact_subnormals(on ? 1 : 0);
+      check(prev);
+      return prev != 0;
+    }
+
     inline int id_of(const std::string& name)
     {
       const int i = bbm_hip_model_id(name.c_str());

@@ -56,6 +56,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <random>
 #include <limits>
 #include <string>
@@ -567,6 +568,46 @@ template<typename CONF>
 using epd_t = bbm::microfacet<bbm::ndf::epd<CONF>, bbm::maskingshadowing::vanginneken<CONF>, bbm::fresnel::complex<CONF>,
                               bbm::microfacet_n::Walter, "EPD">;
 
+// bbm::hip::set_exact_subnormals(true): the adapter's eval + pdf of a Beckmann microfacet model equal the reference's
+// per-pair floats bit for bit on every lane (not only within the per-lane bar)
+template<typename MODEL>
+static bool check_exact(const MODEL& model, size_t n, unsigned seed)
+{
+  using Vec3d = typename MODEL::Vec3d;
+  std::mt19937 rng(seed);
+  std::uniform_real_distribution<float> u(0.0f, 1.0f);
+  std::vector<float> h[6];
+  for(auto& v : h) v.resize(n);
+  for(size_t i = 0; i < n; ++i)
+    for(int k = 0; k < 2; ++k)
+    {
+      float z = u(rng), phi = 6.2831853f * u(rng), s = std::sqrt(std::max(1.0f - z * z, 0.0f));
+      h[3 * k + 0][i] = s * std::cos(phi); h[3 * k + 1][i] = s * std::sin(phi); h[3 * k + 2][i] = z;
+    }
+  std::vector<dev_buf> d;
+  d.reserve(6);
+  for(int k = 0; k < 6; ++k) { d.emplace_back(n); upload(d.back(), h[k]); }
+  dev_buf r(n), g(n), b(n), pdf(n);
+  const bool prev = bbm::hip::set_exact_subnormals(true);
+  bbm::hip::eval_pdf(model, bbm::hip::soa3{d[0].p, d[1].p, d[2].p}, bbm::hip::soa3{d[3].p, d[4].p, d[5].p}, n,
+                     {r.p, g.p, b.p}, pdf.p);
+  HIPCHECK(hipDeviceSynchronize());
+  bbm::hip::set_exact_subnormals(prev);
+  auto R = download(r, n), G = download(g, n), B = download(b, n), P = download(pdf, n);
+  size_t differ = 0;
+  for(size_t i = 0; i < n; ++i)
+  {
+    const Vec3d in(h[0][i], h[1][i], h[2][i]), out(h[3][i], h[4][i], h[5][i]);
+    const auto f = model.eval(in, out);
+    const float p = model.pdf(in, out);
+    const float got[4] = {R[i], G[i], B[i], P[i]}, want[4] = {float(f[0]), float(f[1]), float(f[2]), p};
+    if(std::memcmp(got, want, sizeof(got)) != 0) ++differ;
+  }
+  std::printf("{\"check\": \"exact_subnormals\", \"model\": \"%s\", \"lanes\": %zu, \"lanes_not_bit_identical\": %zu}\n",
+              json_escape(label(model)).c_str(), n, differ);
+  return differ == 0;
+}
+
 int main()
 {
   using F = bbm::floatRGB;
@@ -581,6 +622,8 @@ int main()
     p[0] = 0.2f; p[1] = 0.4f; p[2] = 0.6f; p[3] = 0.35f; p[4] = 2.1f;
   }
   ok &= check_model(ct2, n, seed++);
+  ok &= check_exact(ct, n, seed++);
+  ok &= check_exact(ct2, n, seed++);
   // every other exported analytic model (BBM_EXPORT_BSDFMODEL, include/bsdfmodel/*.h), default attributes
 #define CHECK(T, N) ok &= check_model(T<F>(), N, seed++);
   CHECK(bbm::ggx, n) CHECK(bbm::lambertian, n) CHECK(bbm::cooktorrancewalter, n) CHECK(bbm::lowcooktorrance, n)
