@@ -16,6 +16,23 @@
 #include "math.hpp"
 #include "epd.hpp"      // gamma_q_inv_d
 
+// Round-3 defaults, each with an A/B switch back (tools/build_variant_units.sh), measured per 10 M pairs in
+// tools/gpu_r03_u.sh (profiles/r03_f64_fdiv_ab.txt):
+// * BBM_HIP_F64_FDIV / _MF: the quotients whose operands are provably in range on every lane that keeps its result
+//   (Student-T's G1 rationals, 1 / (1 + lambda) and cotangent, the microfacet scale and pdf divisions, the Cook
+//   Fresnel, Bagher's reciprocals) as div_fast / rsqrt_fast instead of the IEEE sequences -- Ribardiere 0.250 ->
+//   0.220 ms, CookTorrance 0.148 -> 0.144; off with -DBBM_HIP_F64_IEEE_QUOTIENTS
+// * BBM_HIP_F64_VPARAM: Bagher's 27 per-channel parameters pinned in VGPRs -- as kernel arguments they exceeded the
+//   SGPR file and were spilled into VGPR lanes, one v_readlane per use (1 154 of the two-pairs kernel's 6 113 VALU
+//   instructions); Bagher 0.259 -> 0.248 ms; off with -DBBM_HIP_F64_SGPR_PARAMS
+#ifndef BBM_HIP_F64_IEEE_QUOTIENTS
+#define BBM_HIP_F64_FDIV 1
+#define BBM_HIP_F64_FDIV_MF 1
+#endif
+#ifndef BBM_HIP_F64_SGPR_PARAMS
+#define BBM_HIP_F64_VPARAM 1
+#endif
+
 namespace bbmhip {
 namespace f64 {
 
@@ -188,6 +205,30 @@ __device__ __forceinline__ void cossin_phi(d3 v, double& c, double& s)
   c = pole ? 1.0 : fmin(fmax(v.x * r, -1.0), 1.0);
   s = pole ? 0.0 : fmin(fmax(v.y * r, -1.0), 1.0);
 }
+// n / d for a finite d whose reciprocal is a finite normal double (no IEEE special-case handling): the v_rcp_f64 seed,
+// two Newton steps and one remainder correction -- the IEEE quotient or its neighbour (8 instructions against the
+// division sequence's 11).  Only where the operands are provably in range on every lane whose result is used.
+__device__ __forceinline__ double div_fast(double n, double d)
+{
+  double r = __builtin_amdgcn_rcp(d);
+  r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+  const double q = n * r;
+  return __builtin_fma(__builtin_fma(-d, q, n), r, q);
+}
+// 1 / sqrt(x) for a finite normal x > 0: the v_rsq_f64 seed and two Goldschmidt steps (g -> sqrt x, h -> 1 / (2 sqrt x)),
+// within a few ulp of 1.0 / sqrt(x) against ~23 instructions for the IEEE square root and division
+__device__ __forceinline__ double rsqrt_fast(double x)
+{
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g); h = __builtin_fma(h, r, h);
+  r = __builtin_fma(-g, h, 0.5);
+  h = __builtin_fma(h, r, h);
+  return 2.0 * h;
+}
+
 // the native backbone's erfinv (backbone/native/include/backbone/math.h:115-120, Giles' polynomials) in double
 __device__ __forceinline__ double erfinv(double a)
 {
@@ -338,9 +379,11 @@ template<bool Aniso>
 struct StudentT
 {
   static constexpr int kParams = (Aniso ? 2 : 1) + 1;
-  double au, av, gamma, lam_scale, s1_scale, sqrt_g1, f22, f23;
+  double au, av, gamma, lam_scale, s1_scale, sqrt_g1, f22, f23, iau, iav;
   __device__ explicit StudentT(const double* p) : au(p[0]), av(Aniso ? p[1] : p[0]), gamma(p[Aniso ? 2 : 1])
   {
+    iau = 1.0 / au;
+    iav = 1.0 / av;
     // parameter-only factors of G1 (studentt.h:152-156), once per thread
     lam_scale = tgamma(gamma - 0.5) / tgamma(gamma) * kInvSqrtPi;
     s1_scale = pow_d(gamma - 1, gamma) / (2 * gamma - 3);
@@ -351,14 +394,25 @@ struct StudentT
   __device__ __forceinline__ double eval(d3 h) const
   {
     const double z2 = h.z * h.z;
+#ifdef BBM_HIP_F64_FDIV
+    // the roughness quotients as products with hoisted reciprocals (<= 1 ulp apart)
+    const double den = pow_d(1.0 + sqnorm2(h.x * iau, h.y * iav) / ((gamma - 1) * z2), gamma);
+#else
     const double den = pow_d(1.0 + sqnorm2(h.x / au, h.y / av) / ((gamma - 1) * z2), gamma);
+#endif
     const double D = 1.0 / (kPi * (au * av) * (z2 * z2) * den);
     return (h.z > 0) ? D : 0.0;
   }
+#ifdef BBM_HIP_F64_FDIV
+  // F21 / F24 / 1 / (1 + lambda): denominators >= 0.5 on every lane whose G1 is used (z > 0, lambda > -1/2)
+  __device__ __forceinline__ static double qdiv(double n, double d) { return div_fast(n, d); }
+#else
+  __device__ __forceinline__ static double qdiv(double n, double d) { return n / d; }
+#endif
   __device__ __forceinline__ static double F21(double z)
   {
     const double z2 = z * z, z3 = z2 * z;
-    return (1.066 * z + 2.655 * z2 + 4.892 * z3) / (1.038 + 2.969 * z + 4.305 * z2 + 4.418 * z3);
+    return qdiv(1.066 * z + 2.655 * z2 + 4.892 * z3, 1.038 + 2.969 * z + 4.305 * z2 + 4.418 * z3);
   }
   __device__ __forceinline__ static double F22(double g)
   {
@@ -373,18 +427,23 @@ struct StudentT
   __device__ __forceinline__ static double F24(double z)
   {
     const double z2 = z * z, z3 = z2 * z;
-    return (6.537 + 6.074 * z - 0.623 * z2 + 5.223 * z3) / (6.538 + 6.103 * z - 3.218 * z2 + 6.347 * z3);
+    return qdiv(6.537 + 6.074 * z - 0.623 * z2 + 5.223 * z3, 6.538 + 6.103 * z - 3.218 * z2 + 6.347 * z3);
   }
   // studentt.h:128-156
   __device__ __forceinline__ double G1(d3 v, d3 m) const
   {
     const bool mask = (v.z > 0) && (dot(v, m) > 0);
     const bool normal_mask = v.z < 1.0 - kEps;
+#ifdef BBM_HIP_F64_FDIV
+    // |v.xy alpha|^2 >= alpha^2 (1 - (1 - eps)^2) > 0 where normal_mask holds (the only lanes whose lambda is used)
+    const double z = v.z * rsqrt_fast(sqnorm2(v.x * au, v.y * av));
+#else
     const double z = v.z * (1.0 / sqrt(sqnorm2(v.x * au, v.y * av)));
+#endif
     const double S1 = pow_d((gamma - 1) + z * z, 1.5 - gamma) / z;
     const double S2 = F21(z) * (f22 + f23 * F24(z));
     const double lambda = normal_mask ? lam_scale * (s1_scale * S1 + sqrt_g1 * S2) - 0.5 : 0.0;
-    return mask ? (normal_mask ? 1.0 / (1.0 + lambda) : 1.0) : 0.0;
+    return mask ? (normal_mask ? qdiv(1.0, 1.0 + lambda) : 1.0) : 0.0;
   }
   __device__ __forceinline__ double pdf(d3, d3 m, double D) const
   {
@@ -504,8 +563,14 @@ struct FresnelCook
   __device__ __forceinline__ double eval(double c) const
   {
     const double g = safe_sqrt(eta * eta + c * c - 1.0);
+#ifdef BBM_HIP_F64_FDIV_MF
+    // eta >= 1: g >= |c|, so g + c >= 0 and c (g - c) + 1 >= 1 - c^2 + c g > 0 for c in [0, 1] (0 / 0 -> NaN either way)
+    const double a = div_fast(g - c, g + c);
+    const double b = div_fast(c * (g + c) - 1.0, c * (g - c) + 1.0);
+#else
     const double a = (g - c) / (g + c);
     const double b = (c * (g + c) - 1.0) / (c * (g - c) + 1.0);
+#endif
     return fmax(0.5 * (a * a) * (1.0 + b * b), 0.0);
   }
 };
@@ -547,16 +612,26 @@ struct Microfacet
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
     const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
+    // the halfway vector keeps the IEEE 1 / sqrt: a last-ulp h.z above 1 (in + out along z) would make 1 - z^2 < 0
     const d3 h = normalize(mk(in.x + out.x, in.y + out.y, in.z + out.z));
     const double D = ndf.eval(h);
     const double inh = dot(in, h), outh = dot(out, h);
     const double G = MS::eval(ndf, in, out, h, inh, outh);
     const double F = fresnel.eval(0.5 * (inh + outh));
+#ifdef BBM_HIP_F64_FDIV_MF
+    // z_in z_out > 0 and |out.h| > 0 on active lanes (the only ones whose results are kept); the pdf's 0 / 0 where
+    // out.h = 0 stays NaN either way
+    const double res = div_fast(D * G * F / norm_value<N>::v, in.z * out.z);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = active ? (Scaled ? res * albedo[c] : res) : 0.0;
+    pdf = active ? div_fast(ndf_pdf<NDF>::run(ndf, out, h, D), 4.0 * fabs(outh)) : 0.0;
+#else
     const double res = D * G * F / norm_value<N>::v / (in.z * out.z);
 #pragma unroll
     for (int c = 0; c < 3; ++c) rgb[c] = active ? (Scaled ? res * albedo[c] : res) : 0.0;
     // the pdf's `h = z(h) < 0 ? -h : h` (:167) never fires on active lanes
     pdf = active ? ndf_pdf<NDF>::run(ndf, out, h, D) / (4.0 * fabs(outh)) : 0.0;
+#endif
   }
 
   // :115-141: m ~ NDF sample(out), direction = reflect(out, m) = m (m.out) 2.0 - out (core/vec_transform.h:43-44),
@@ -1142,6 +1217,15 @@ struct Bagher
     hc_min = fmin(fmin(hc0[0], hc0[1]), hc0[2]);
     ggx.au = ggx.av = (((0.0 + alpha[0]) + alpha[1]) + alpha[2]) / 3;
     ggx.iau = ggx.iav = 1.0 / ggx.au;
+#ifdef BBM_HIP_F64_VPARAM
+    // an empty asm with a VGPR operand: the value stays in a VGPR (no SGPR copy to spill and read back per use)
+    for (int j = 0; j < 3; ++j)
+    {
+      asm("" : "+v"(albedo[j])); asm("" : "+v"(K[j])); asm("" : "+v"(Lambda[j])); asm("" : "+v"(c[j]));
+      asm("" : "+v"(theta0[j])); asm("" : "+v"(k[j])); asm("" : "+v"(F0[j])); asm("" : "+v"(F1[j]));
+      asm("" : "+v"(p[j]));
+    }
+#endif
   }
   // sgd.h:185-190 G1 for an upper-hemisphere direction with squared chord hc (theta = 2 asin(sqrt(hc) / 2)): the
   // branch skips the shadowing term (a log and two exponentials) where theta <= theta0; th is theta_of(v),
@@ -1176,7 +1260,12 @@ struct Bagher
     // the quotients by per-channel constants and by the pair's common denominators as products with one
     // reciprocal each (<= 2 ulp apart from the reference's quotients), and sgd.h:58-59's
     // exp(-t) / pow(t, p) as one exponential e^(-t - p ln t) on log2_d (den > eps <=> p log2 t > -52)
+#ifdef BBM_HIP_F64_FDIV_MF
+    // dnorm > 0 where h.z > 0 and z_in z_out > 0 on active lanes; other lanes are selected away
+    const double inv_dnorm = div_fast(1.0, dnorm), inv_cos = div_fast(1.0, kPi * (in.z * out.z));
+#else
     const double inv_dnorm = 1.0 / dnorm, inv_cos = 1.0 / (kPi * (in.z * out.z));
+#endif
 #pragma unroll
     for (int j = 0; j < 3; ++j)
     {
@@ -1194,7 +1283,11 @@ struct Bagher
       const double res = Dj * Gj * Fj * inv_cos;
       rgb[j] = active ? res * albedo[j] : 0.0;
     }
+#ifdef BBM_HIP_F64_FDIV_MF
+    pdf = active ? div_fast(vndf_pdf(ggx, out, h, ggx.eval(h)), 4.0 * fabs(outh)) : 0.0;
+#else
     pdf = active ? vndf_pdf(ggx, out, h, ggx.eval(h)) / (4.0 * fabs(outh)) : 0.0;
+#endif
   }
   __device__ __forceinline__ void reflectance(d3 out, uint32_t component, double* rgb) const
   {
