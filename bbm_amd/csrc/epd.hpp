@@ -49,7 +49,15 @@ __device__ __forceinline__ float epd_g1_lookup(const float* tab, float p, float 
   // instructions each): m1 only places the bilinear weights, which are continuous across a floor() flip, so an
   // m1 within 1e-12 of the reference's moves the interpolated G1 by ~1e-12 relative
   // (L = +-inf at t = 0 / inf: the reference's exp(-exp(L 0.05)) is 0 / 1, exp_dd's polynomial would give NaN)
+#ifdef BBM_HIP_EPD_LOGF_CR
   const double L = double(logf_cr(div_nr(1.0f, t)));
+#else
+  // ln(1 / t) from log2_acc (~2^-44 absolute) instead of the library's double log: like m1's exponentials it only
+  // places the bilinear weights, continuously (dm1/dL <= ~18.4), so ~1e-13 in L moves G1 by ~1e-12 relative
+  const float it = div_nr(1.0f, t);
+  const double L = (it == 0.0f) ? -__builtin_inf() : ((it > 3.40282347e38f) ? __builtin_inf()
+                   : ((it != it) ? double(it) : double(float(log2_acc(it) * 0.69314718055994530942))));
+#endif
   const double e1 = __builtin_isfinite(L) ? exp_dd(-exp_dd(L * 0.05)) : ((L > 0.0) ? 0.0 : 1.0);
   const double m1 = (L != L) ? L : e1 * 1000.0 - 1.0;        // NaN stays NaN
 #endif
