@@ -1,10 +1,10 @@
 #!/bin/bash
-# floatRGB EPD: the G1 index map's ln(1/t) from log2_acc (default) vs the library's double log (epdlog); EPD parity
+# floatRGB EPD: Van Ginneken azimuths from the f32 atan2 (default) vs the double atan2 rounded to float (phicr); EPD parity
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/x
 for round in 1 2 3; do
-  for V in default epdlog; do
+  for V in default phicr; do
     lib=""; [ "$V" = default ] || lib="BBM_HIP_LIB=bbm_amd/lib_ab/$V/libbbm_hip.so"
     env $lib timeout -k 10 200 python bench.py --workload models --models EPD,CookTorranceHeitz --steps 5 --warmup 2 > gpurun_out/m.json 2>gpurun_out/m.err || { echo "models $V failed"; tail gpurun_out/m.err; exit 1; }
     python3 -c "
