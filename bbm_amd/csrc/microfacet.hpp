@@ -165,7 +165,13 @@ struct PhongNdf
   __device__ __forceinline__ float G1(v3 v, v3 m) const
   {
     const bool mask = (v.z > 0) && (dot3(v, m) > 0);
+#ifdef BBM_HIP_PHONG_G1_IEEE
     const float a = float(sqrt(0.5 * sharpness + 1) / double(tan_theta(v)));
+#else
+    // the double quotient rounded to float as f_div_d (f32 seed + one f64 remainder step: the same float but within
+    // ~2^-21 ulp of a midpoint) instead of the IEEE double division sequence
+    const float a = f_div_d(sqrt(0.5 * sharpness + 1), double(tan_theta(v)));
+#endif
     const double ad = a;
     const float g = f_div_d(3.535 * ad + 2.181 * ad * ad, 1 + 2.276 * ad + 2.577 * ad * ad);
     return mask ? ((a < 1.6) ? g : 1.0f) : 0.0f;
