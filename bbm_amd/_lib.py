@@ -69,10 +69,11 @@ SIGNATURES = {
     "bbm_hip_aggregate_sample_f64": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P, _P, _P]),
     "bbm_hip_aggregate_reflectance_f64": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _U32, _U32, _P, _P, _P, _P]),
     "bbm_hip_scratch_trim": (_SZ, []),
+    "bbm_hip_scratch_trim_captured": (_SZ, []),
     "bbm_hip_scratch_bytes": (_SZ, []),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
 
 

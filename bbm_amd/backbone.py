@@ -646,6 +646,12 @@ def scratch_trim():
     return int(_lib.load().bbm_hip_scratch_trim())
 
 
+def scratch_trim_captured():
+    """Free the scratch blocks that HIP-graph captures of library calls hold (bbm_hip_scratch_trim_captured): only
+    once every such graph is destroyed.  Returns the bytes freed."""
+    return int(_lib.load().bbm_hip_scratch_trim_captured())
+
+
 def scratch_bytes():
     """Device bytes the library's scratch pool currently holds (bbm_hip_scratch_bytes)."""
     return int(_lib.load().bbm_hip_scratch_bytes())

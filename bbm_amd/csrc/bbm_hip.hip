@@ -36,6 +36,8 @@ struct ScratchBlock
   hipEvent_t released;     // recorded on `last` when the block was released
   hipStream_t last;
   bool busy, used;
+  bool pinned;             // handed out while `last` was capturing a graph: the graph keeps the address, so the
+                           // block is never handed out or freed again (bbm_hip_scratch_trim_captured aside)
 };
 std::mutex g_scratch_mu;
 std::vector<ScratchBlock> g_scratch;
@@ -61,7 +63,7 @@ size_t free_idle(bool wait, size_t keep)
   for (size_t i = g_scratch.size(); i-- > 0 && idle > keep;)
   {
     ScratchBlock& b = g_scratch[i];
-    if (b.busy) continue;
+    if (b.busy || b.pinned) continue;
     if (b.used && (wait ? hipEventSynchronize(b.released) : hipEventQuery(b.released)) != hipSuccess) continue;
     (void)hipFree(b.p);
     (void)hipEventDestroy(b.released);
@@ -79,11 +81,27 @@ void* scratch_acquire(size_t bytes, hipStream_t s)
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   bytes = (bytes + 255) & ~size_t(255);
   std::lock_guard<std::mutex> lock(g_scratch_mu);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return nullptr;
+  if (cap != hipStreamCaptureStatusNone)
+  {
+    // graph capture: a fresh block that belongs to the graph from now on.  No idle block is reused (its release
+    // event was recorded outside the capture, and waiting on it would tie the graph to a pre-capture event), and
+    // the allocation runs in relaxed capture mode (hipMalloc is not allowed under a global-mode capture).
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    ScratchBlock b{nullptr, bytes, dev, nullptr, s, true, true, true};
+    const bool ok = hipMalloc(&b.p, bytes) == hipSuccess;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (!ok) return nullptr;
+    g_scratch.push_back(b);
+    return b.p;
+  }
   // best fit among idle blocks of this device, but not one much larger than the request (a 360-byte CDF must not
   // pin a block sized for 125M lanes)
   ScratchBlock* best = nullptr;
   for (ScratchBlock& b : g_scratch)
-    if (!b.busy && b.device == dev && b.bytes >= bytes && (b.bytes <= 4 * bytes || b.bytes - bytes <= (size_t(1) << 20)) &&
+    if (!b.busy && !b.pinned && b.device == dev && b.bytes >= bytes && (b.bytes <= 4 * bytes || b.bytes - bytes <= (size_t(1) << 20)) &&
         (!best || b.bytes < best->bytes))
       best = &b;
   if (best)
@@ -94,7 +112,7 @@ void* scratch_acquire(size_t bytes, hipStream_t s)
     best->busy = true;
     return best->p;
   }
-  ScratchBlock b{nullptr, bytes, dev, nullptr, s, true, false};
+  ScratchBlock b{nullptr, bytes, dev, nullptr, s, true, false, false};
   if (hipMalloc(&b.p, bytes) != hipSuccess)
   {
     // out of device memory: return every idle block (after its last use) and try once more
@@ -117,19 +135,43 @@ void scratch_release(void* p, hipStream_t s)
   for (ScratchBlock& b : g_scratch)
     if (b.p == p)
     {
+      if (b.pinned) return;      // the captured graph owns it: no event, no reuse, and no freeing inside a capture
       (void)hipEventRecord(b.released, s);
       b.last = s;
       b.busy = false;
       b.used = true;
       break;
     }
-  free_idle(false, retain_limit());
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) free_idle(false, retain_limit());
 }
 
 size_t scratch_trim()
 {
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   return free_idle(true, 0);
+}
+
+size_t scratch_trim_captured()
+{
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  size_t freed = 0;
+  bool synced = false;
+  for (size_t i = g_scratch.size(); i-- > 0;)
+  {
+    ScratchBlock& b = g_scratch[i];
+    if (!b.pinned) continue;
+    if (!synced)
+    {
+      (void)hipDeviceSynchronize();
+      synced = true;
+    }
+    (void)hipFree(b.p);
+    if (b.released) (void)hipEventDestroy(b.released);
+    freed += b.bytes;
+    g_scratch.erase(g_scratch.begin() + long(i));
+  }
+  return freed + free_idle(true, 0);
 }
 
 size_t scratch_bytes()
@@ -532,6 +574,8 @@ int bbm_hip_abi_version(void) { return BBM_HIP_ABI_VERSION; }
 int bbm_hip_set_exact_subnormals(int on) { return exact_subnormals().exchange(on != 0 ? 1 : 0); }
 
 size_t bbm_hip_scratch_trim(void) { return scratch_trim(); }
+
+size_t bbm_hip_scratch_trim_captured(void) { return scratch_trim_captured(); }
 
 size_t bbm_hip_scratch_bytes(void) { return scratch_bytes(); }
 

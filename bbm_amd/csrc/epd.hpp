@@ -206,7 +206,7 @@ struct EpdNdf
     float sp, cp;
     cossin_cr(kPi2F * xi0, cp, sp);
     const float g = float(gamma_q_inv_d(double(inv_p), double(xi1)));
-    const float tan2 = beta * beta * powf_acc(g, inv_p);
+    const float tan2 = beta * beta * powf_glibc(g, inv_p);      // glibc powf (epd.h:100)
     const float cosT = float(1.0 / sqrt(1.0 + double(tan2)));          // rsqrt(1.0 + tan2) in double, stored as Value
     const float sinT = float(safe_sqrt(1.0 - double(cosT * cosT)));
     return mk3(cp * sinT, sp * sinT, cosT);

@@ -215,7 +215,7 @@ struct He
     const float f0 = div_nr(1.0f, sqrtf(kPi8F)) * (Ki + Ko);
     // safe_sqrt(2.0 * log(f0)): 2 x a float is exact in float and double alike, and a correctly rounded double
     // sqrt rounded to float is the correctly rounded float sqrt (53 >= 2 x 24 + 2): identical, without the f64 sqrt
-    float x = (f0 <= 1.0f) ? f0 : safe_sqrtf(2.0f * logf_cr(f0));
+    float x = (f0 <= 1.0f) ? f0 : safe_sqrtf(2.0f * logf_glibc(f0));
 #pragma unroll
     for (int s = 0; s < 4; ++s)
     {

@@ -42,9 +42,9 @@ __global__ __launch_bounds__(256) void k_epd_p2(const float* __restrict__ dq, co
   for (int i = 0; i < nq; ++i)
   {
     const float qi = q[i];
-    // glibc's expf / powf (what the generator called) are correctly rounded but for rare cases: rounding the
-    // f64 results reproduces them; the device's ~1-ulp f32 versions would perturb the cancelling recurrence
-    integral += dq[i] * expf_cr(-powf_cr(r2 + qi * qi, p));
+    // glibc's expf / powf, what the generator called (G1.cpp:91-223 on x86-64), restated bit for bit (math.hpp):
+    // the device's ~1-ulp f32 versions, or even the correctly rounded floats, would perturb the summation
+    integral += dq[i] * expf_glibc(-powf_glibc(r2 + qi * qi, p));
   }
   out[row * kEpdCols + j] = float(2.0 * double(norm[row]) * double(integral));
 }

@@ -319,14 +319,19 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
 // k_eval_pdf_compact, which evaluates only the live pairs, packed densely into waves.
 template<class Model> struct compact_eval { static constexpr bool value = false; };
 
-// Compaction on/off (BBM_HIP_COMPACT=0 disables; A/B experiments).
+// Compaction on/off.  The shipped library always compacts; only an experimental build (BBM_HIP_EXPERIMENTAL, A/B
+// runs) reads BBM_HIP_COMPACT=0 from the environment, so a user's environment cannot change which kernel runs.
 inline bool use_compact()
 {
+#ifdef BBM_HIP_EXPERIMENTAL
   static const bool v = [] {
     const char* e = std::getenv("BBM_HIP_COMPACT");
     return e ? std::atoi(e) != 0 : true;
   }();
   return v;
+#else
+  return true;
+#endif
 }
 
 // Stream compaction of live pairs before evaluation.  A wave executes the slowest of its 64 lanes: for a
@@ -518,7 +523,10 @@ __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compac
   }
 }
 
-// Grid cap for the grid-stride kernels; BBM_HIP_MAX_BLOCKS overrides it (tuning experiments).
+// Grid cap for the grid-stride kernels.  Launch-variant knobs (BBM_HIP_MAX_BLOCKS, BBM_HIP_PPT = 8 pairs per thread,
+// BBM_HIP_PIPE = the software-pipelined kernel, BBM_HIP_NT = 0 temporal loads / stores) exist only in an
+// experimental build (-DBBM_HIP_EXPERIMENTAL, tools/build_variant.sh): the shipped library reads no tuning knob.
+#ifdef BBM_HIP_EXPERIMENTAL
 inline uint64_t max_blocks()
 {
   static const uint64_t v = [] {
@@ -529,7 +537,6 @@ inline uint64_t max_blocks()
   return v;
 }
 
-// Pairs per thread of the vector kernel (BBM_HIP_PPT=8 selects k_eval_pdf_v8; tuning experiments).
 inline int pairs_per_thread()
 {
   static const int v = [] {
@@ -539,7 +546,6 @@ inline int pairs_per_thread()
   return v;
 }
 
-// Software-pipelined grid-stride kernel (BBM_HIP_PIPE=1; tuning experiments).
 inline bool use_pipe()
 {
   static const bool v = [] {
@@ -549,7 +555,6 @@ inline bool use_pipe()
   return v;
 }
 
-// Streaming stores/loads with the nontemporal hint (BBM_HIP_NT=0 disables; tuning experiments).
 inline bool use_nt()
 {
   static const bool v = [] {
@@ -558,6 +563,9 @@ inline bool use_nt()
   }();
   return v;
 }
+#else
+constexpr uint64_t max_blocks() { return uint64_t(kMaxBlocks); }
+#endif
 
 // ------------------------------------------------------------------------------- sample
 

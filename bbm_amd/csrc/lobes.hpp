@@ -184,7 +184,7 @@ struct Lafortune
       : cx(p[3]), cy(Aniso ? p[4] : p[3]), cz(p[Aniso ? 5 : 4]), s(p[Aniso ? 6 : 5])
   {
     albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2];
-    ngan = NGAN ? (s + 2.0) * kInvPiHalfF / double(powf_cr(fmaxf(cz * cz, cx * cx), s * 0.5f)) : 1.0;   // glibc powf
+    ngan = NGAN ? (s + 2.0) * kInvPiHalfF / double(powf_glibc(fmaxf(cz * cz, cx * cx), s * 0.5f)) : 1.0;   // glibc powf
   }
 
   template<int MODE>
@@ -220,7 +220,7 @@ struct Lafortune
   {
     const bool m = component & kFlagSpecular;
     const v3 co = mk3(cx * out.x, cy * out.y, cz * out.z);
-    const float nrm = powf_cr(sqrtf(dot3(co, co)), s) * kPi2F;
+    const float nrm = powf_glibc(sqrtf(dot3(co, co)), s) * kPi2F;
     const float normalization = div_nr(nrm, s + 2);
 #pragma unroll
     for (int c = 0; c < 3; ++c)
@@ -509,8 +509,8 @@ struct LowSmooth
   __device__ __forceinline__ void reflectance(v3 out, uint32_t component, float* rgb) const
   {
     const bool m = (component & kFlagSpecular) && (out.z > 0);
-    const float f1 = div_nr(logf_cr(B + 1), 2 * B);
-    const float f2 = float((1.0 - double(powf_cr(B + 1, 1 - C))) / double(2 * B * (C - 1)));
+    const float f1 = div_nr(logf_glibc(B + 1), 2 * B);
+    const float f2 = float((1.0 - double(powf_glibc(B + 1, 1 - C))) / double(2 * B * (C - 1)));
     const float factor = (fabsf(C - 1) < kEpsF) ? f1 : f2;
     const float q = div_nr(fres.eta - 1, fres.eta + 1);
     const float R0 = q * q;
@@ -526,9 +526,9 @@ struct LowSmooth
     const float ro2 = sin_theta2(out);
     const float bb = B * (1 - ro2);
     float temp = float(1.0 + (2 * B * (1.0 + ro2)) + double(bb * bb));
-    temp = float(-log(2.0) + double(logf_cr(1 + B * (1 - ro2) + safe_sqrtf(temp))));
+    temp = float(-log(2.0) + double(logf_glibc(1 + B * (1 - ro2) + safe_sqrtf(temp))));
     const float mdpi = B * div_nr(1.0f, temp);
-    const float E = float(2.0 * double(expf_cr(xi0 * B * div_nr(1.0f, mdpi))));
+    const float E = float(2.0 * double(expf_glibc(xi0 * B * div_nr(1.0f, mdpi))));
     const float ri = safe_sqrtf(div_nr((E - 2) * (E + 2 * B * ro2), 2 * E * B));
     const float ro = sqrtf(ro2);
     const double rp = double(ri + ro), rm = double(ri - ro);

@@ -303,6 +303,95 @@ __device__ __forceinline__ float expf_glibc_neg(float x)
   return (x < -0x1.9fe368p6f) ? 0.0f : res;
 }
 
+// glibc 2.35's logf and powf (sysdeps/ieee754/flt-32/e_logf.c, e_powf.c with e_logf_data.c, e_powf_log2_data.c and
+// e_exp2f_data.c -- the Arm optimized-routines algorithms behind the reference's bbm::log(float) / bbm::pow(float,
+// float) -> std::log / std::pow -> logf / powf on x86-64), restated in IEEE double ops as the FMA-contracted ifunc
+// variant the host runs.  Neither is correctly rounded (logf 0.82 ulp; powf carries up to 1.27 2^-26 relative error
+// into its one rounding, so ~0.1 % of its results are not the nearest float), and where the reference cancels
+// right after (Bagher's 1 - e^(c theta^k)) only glibc's own float reproduces its result.  The tables and polynomials
+// are glibc's data (as in this machine's libm.so.6), not the reference's.  Both are pinned to the host libm by
+// oracle/glibcf_check.c: logf on every positive float, powf on 1e9 random pairs -- 0 mismatches.
+__device__ __constant__ const double kLogfTab[16][2] = {    // {1/c, log c}
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5}, {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+__device__ __constant__ const double kPowfLog2Tab[16][2] = {    // {1/c, log2 c}
+    {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2}, {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2},
+    {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2}, {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2},
+    {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2}, {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3}, {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4},
+    {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4}, {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3},
+    {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
+    {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2}, {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}};
+
+// x = 2^k z with z in [0x3f330000, 2 x 0x3f330000): the bits of z, k, and the table row (subnormal x normalised)
+__device__ __forceinline__ uint32_t glibcf_reduce(float x, uint32_t& i, int& k)
+{
+  const uint32_t ix0 = __float_as_uint(x);
+  const uint32_t ix = (ix0 < 0x00800000u) ? ((__float_as_uint(x * 0x1p23f) & 0x7fffffffu) - (23u << 23)) : ix0;
+  const uint32_t tmp = ix - 0x3f330000u;
+  i = (tmp >> 19) & 15u;
+  k = int32_t(tmp) >> 23;
+  return ix - (tmp & 0xff800000u);
+}
+
+__device__ __forceinline__ float logf_glibc(float x)
+{
+  uint32_t i;
+  int k;
+  const double z = double(__uint_as_float(glibcf_reduce(x, i, k)));
+  const double r = __builtin_fma(z, kLogfTab[i][0], -1.0);
+  const double y0 = __builtin_fma(double(k), 0x1.62e42fefa39efp-1, kLogfTab[i][1]);
+  const double r2 = r * r;
+  double y = __builtin_fma(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
+  y = __builtin_fma(-0x1.00ea348b88334p-2, r2, y);
+  y = __builtin_fma(y, r2, y0 + r);
+  float res = float(y);                                           // x = 1: exactly +0
+  res = (x == __builtin_inff()) ? x : res;
+  res = (x == 0.0f) ? -__builtin_inff() : res;
+  return (x < 0.0f || x != x) ? __builtin_nanf("") : res;
+}
+
+// powf for x >= 0 (or NaN), any y (the reference's uses: a distance or a sum of squares to a parameter power)
+__device__ __forceinline__ float powf_glibc(float x, float y)
+{
+  uint32_t i;
+  int k;
+  const double z = double(__uint_as_float(glibcf_reduce(x, i, k)));
+  const double r = __builtin_fma(z, kPowfLog2Tab[i][0], -1.0);
+  const double y0 = kPowfLog2Tab[i][1] + double(k);
+  const double r2 = r * r;
+  double q0 = __builtin_fma(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
+  const double p = __builtin_fma(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+  const double r4 = r2 * r2;
+  double q = __builtin_fma(0x1.71547652ab82bp+0, r, y0);
+  q = __builtin_fma(p, r2, q);
+  const double ylogx = double(y) * __builtin_fma(q0, r4, q);      // log2(x) y
+  // 2^ylogx: k/32 + rr, 2^(k/32) from expf's table, a cubic in rr
+  constexpr double kShift = 0x1.8p+52 / 32;
+  const double kb = ylogx + kShift;
+  const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
+  const double rr = ylogx - (kb - kShift);
+  const double s = __builtin_bit_cast(double, expf_tab(uint32_t(ki) & 31u) + (ki << 47));
+  const double zz = __builtin_fma(0x1.c6af84b912394p-5, rr, 0x1.ebfce50fac4f3p-3);
+  double e = __builtin_fma(0x1.62e42ff0c52d6p-1, rr, 1.0);
+  e = __builtin_fma(zz, rr * rr, e);
+  float res = float(e * s);
+  res = (ylogx > 0x1.fffffffd1d571p+6) ? __builtin_inff() : res;
+  res = (ylogx <= -150.0) ? 0.0f : res;
+  // special operands: pow(0, y) = 0 / inf, pow(inf, y) = inf / 0, NaN, pow(x, 0) = pow(1, y) = 1
+  res = (x == 0.0f) ? ((y < 0.0f) ? __builtin_inff() : 0.0f) : res;
+  res = (x == __builtin_inff()) ? ((y < 0.0f) ? 0.0f : __builtin_inff()) : res;
+  res = (x != x || y != y || x < 0.0f) ? __builtin_nanf("") : res;
+  return (y == 0.0f || x == 1.0f) ? 1.0f : res;
+}
+
 // a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
 // q = a rm corrected once by the exact remainder -- the correctly rounded quotient (as div_nr) without v_rcp_f32
 __device__ __forceinline__ float div_small(float a, float m, float rm)

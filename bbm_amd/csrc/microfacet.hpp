@@ -202,7 +202,7 @@ struct StudentT
   __device__ explicit StudentT(const float* p) : au(p[0]), av(Aniso ? p[1] : p[0]), gamma(p[Aniso ? 2 : 1])
   {
     lam_scale = tgamma(gamma - 0.5) / double(tgammaf(gamma)) * kInvSqrtPiF;
-    s1_scale = div_nr(powf_cr(gamma - 1, gamma), 2 * gamma - 3);
+    s1_scale = div_nr(powf_glibc(gamma - 1, gamma), 2 * gamma - 3);
     sqrt_g1 = sqrtf(gamma - 1);
     f22 = F22(gamma);
     f23 = F23(gamma);

@@ -64,10 +64,11 @@ struct Bagher
   __device__ __forceinline__ float G1(int j, float th) const
   {
     // 1 + Lambda (1 - exp(c pow(...))) cancels catastrophically for published fits (fits/bagher_sgd.fit:
-    // k ~ 48, c ~ 1e-7 -> g ~ 5e-4 at grazing angles): pow and theta must round like the reference's
-    // (pow rounded from f64 exp(k log d), which is the correctly rounded powf; powf_xlog's domain holds: d > 0 where
-    // the result is used, and the fit bounds keep k > 0)
-    const float g = 1.0f + Lambda[j] * (1.0f - expf_acc(c[j] * powf_xlog(th - theta0[j], k[j])));
+    // k ~ 48, c ~ 1e-7 -> g ~ 5e-4 at grazing angles): theta, pow and exp must be the reference's own floats --
+    // glibc's powf and expf restated bit for bit (math.hpp; the correctly rounded power differs from glibc's on ~0.1 %
+    // of the lanes, and each such lane moved G by up to 1e-2 relative).  th - theta0 may be <= 0 on lanes the select
+    // below discards.
+    const float g = 1.0f + Lambda[j] * (1.0f - expf_glibc(c[j] * powf_glibc(th - theta0[j], k[j])));
     return (th > theta0[j]) ? g : 1.0f;
   }
   // the same for an upper-hemisphere direction with squared chord q: lanes below the conservative threshold have

@@ -221,14 +221,15 @@ def main(argv=None):
         bpp = BYTES_PER_PAIR_MODEL.get(args.model, BYTES_PER_PAIR)
         achieved = bpp * n / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if os.path.exists(TRAFFIC_FILE):
+        for tf in (os.path.join(ROOT, "profiles", f"traffic_{args.model}.json"), TRAFFIC_FILE):
             try:
-                with open(TRAFFIC_FILE) as f:
+                with open(tf) as f:
                     tr = json.load(f)
-                if tr.get("model") == args.model and tr.get("pairs") == n:
-                    traffic = tr.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
-                traffic = None
+                continue
+            if tr.get("model") == args.model and tr.get("pairs") == n:
+                traffic = tr.get("hbm_bytes_per_launch")
+                break
         line = {
             "metric": METRIC if args.model == "CookTorrance" else f"BSDF evals/s (eval+pdf), {args.model}",
             "value": total_pairs / elapsed,

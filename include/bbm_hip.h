@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 9
+#define BBM_HIP_ABI_VERSION 10
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -243,6 +243,12 @@ int bbm_hip_parse_model_tree(const char* str, int* model_ids, int* nchildren, fl
  * also frees idle blocks by itself beyond BBM_HIP_SCRATCH_RETAIN_MB (default 1024) of retained memory and when
  * an allocation fails.  Returns the bytes freed. */
 size_t bbm_hip_scratch_trim(void);
+/* Blocks handed out while the launch stream was capturing a HIP graph belong to that graph: the pool never reuses
+ * or frees them (a replay writes to them), and neither bbm_hip_scratch_trim nor the pool's own trimming touches
+ * them.  Once every such graph is destroyed, this frees them too (after a device synchronisation) and then trims
+ * like bbm_hip_scratch_trim.  Calling it while a graph that used library scratch may still replay is an error
+ * the library cannot detect.  Returns the bytes freed. */
+size_t bbm_hip_scratch_trim_captured(void);
 /* Bytes the pool currently holds (idle + in use). */
 size_t bbm_hip_scratch_bytes(void);
 

@@ -155,3 +155,43 @@ def test_scratch_reuse_across_streams(bbm):
     torch.cuda.synchronize()
     for k, rgb, pdf, refl, _ in got:
         assert torch.equal(rgb, want[k][0]) and torch.equal(pdf, want[k][1]) and torch.equal(refl, want[k][2]), k
+
+
+def test_scratch_held_by_captured_graph(bbm):
+    """A HIP graph that captured library calls using scratch (a composed aggregate's per-lane terms, He's sampler
+    CDF) keeps those blocks: the pool pins them at capture, so scratch_trim and later uncaptured calls -- which
+    would otherwise free or reuse them -- leave the graph's replays correct."""
+    n = 1 << 16
+    din = bbm.fill_directions(13, 0, 0, n, mode=1)
+    dout = bbm.fill_directions(13, 1, 0, n, mode=1)
+    models = [bbm.Aggregate(bbm.CookTorrance(), bbm.GGX(), bbm.Lambertian(), fused=False), bbm.BsdfModel("HeWestin")]
+    want, outs = [], []
+    for m in models:
+        rgb, pdf = m.eval_pdf(din, dout)
+        torch.cuda.synchronize()
+        want.append((rgb.clone(), pdf.clone()))
+        outs.append((torch.empty_like(rgb), torch.empty_like(pdf)))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        for m, (r, p) in zip(models, outs):
+            m.eval_pdf(din, dout, rgb=r, pdf=p, stream=side)
+    torch.cuda.synchronize()
+    held = bbm.scratch_bytes()
+    bbm.scratch_trim()
+    assert bbm.scratch_bytes() > 0 and bbm.scratch_bytes() <= held
+    # uncaptured calls of other sizes in between: they must not be handed the graph's blocks
+    for m in models:
+        m.eval_pdf(dout[:, : n // 2], din[:, : n // 2])
+    for _ in range(2):
+        for r, p in outs:
+            r.zero_()
+            p.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for (r, p), (wr, wp) in zip(outs, want):
+            assert torch.equal(r, wr) and torch.equal(p, wp)
+    del g
+    torch.cuda.synchronize()
+    bbm.scratch_trim_captured()

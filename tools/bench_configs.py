@@ -51,7 +51,7 @@ def _subset(args, names):
 def valu_roofline(key, kernel_ms, units):
     """VALU roofline of one workload's dominant kernel: its VALU instructions per unit come from the committed
     counter summary (profiles/pmc_valu.json, tools/valu_roofline.py: SQ_INSTS_VALU x 64 lanes / units per
-    dispatch, collected by tools/gpu_pmc_workload.sh), its time from this run's HIP events.  achieved = issued
+    dispatch, collected by tools/gpu_step.sh pmc:...), its time from this run's HIP events.  achieved = issued
     lane-instructions/s x 2 (an FMA's two flops: the unit the 157.3 TFLOP/s f32 vector peak is quoted in), so
     frac = the fraction of the chip's VALU issue slots this kernel fills (an upper bound on its FLOP fraction)."""
     entry = None
@@ -137,13 +137,21 @@ def bench_models(args, dist, rank, world):
             din, dout, rgb = sets[cyc[0] % MODEL_SETS]
             cyc[0] += 1
             m.eval_pdf(din, dout, rgb=rgb, mode=1, stream=s)
-        graph = _graph(launch, reps)
-        elapsed, step_ms = _timed(graph.replay, args, dist, stream)
+        if args.graph == "off":
+            # counter passes (rocprofv3 --pmc serialises dispatches): the same launches issued one by one
+            step = lambda: [launch(stream) for _ in range(reps)]   # noqa: E731
+        else:
+            step = _graph(launch, reps).replay
+        elapsed, step_ms = _timed(step, args, dist, stream)
         kern_ms = step_ms / reps
         bpp = 20 if name in Z_ONLY else 36
         gbs = bpp * n / (kern_ms * 1e-3) / 1e9
         per[name] = {"pairs_per_s": n * world * args.steps * reps / elapsed, "kernel_ms": kern_ms, "GB_s": gbs,
                      "roofline_frac": gbs / HBM_PEAK_GBS, "bytes_per_pair": bpp}
+        vr = valu_roofline(f"models:{name}", kern_ms, n)
+        if vr["frac"] is not None:
+            # VALU-bound models: the fraction of the chip's VALU issue slots, from committed counters of this kernel
+            per[name]["valu_roofline"] = vr
         total_t += elapsed / reps
     if rank == 0:
         _line(args, world, "BSDF evals/s (eval), all single bsdfmodels, 10M shared pairs per GPU (config 3)",

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Build profiles/pmc_valu.json (the VALU counter summaries bench.py's config-4/5 rooflines read) from
-tools/gpu_pmc_workload.sh / tools/gpu_he_pmc.sh output:
+tools/gpu_step.sh pmc:... output:
 
     python tools/valu_roofline.py gpurun_out/pmc_sample:sample:125000000 gpurun_out/pmc_fit:fit:52488000 \
         gpurun_out/pmc_he_after:evalpdf:10000000 > profiles/pmc_valu.json
+    python tools/valu_roofline.py --merge profiles/pmc_valu.json profiles/r04_pmc_models:models:10000000 > new.json
 
 Each argument is <dir>:<workload>:<units per dispatch>; every <dir>/<model>.json (tools/pmc_summary.py output for
 the workload's kernel) becomes workloads["<workload>:<model>"] with
@@ -22,6 +23,10 @@ ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9
 def main(specs):
     out = {"peak_tflops": 157.3, "issue_peak_wave_instr_per_s": ISSUE_PEAK,
            "definition": __doc__.strip().split("\n\n")[-1], "workloads": {}}
+    if specs and specs[0] == "--merge":       # keep an existing summary's workloads, replace / add the given ones
+        with open(specs[1]) as f:
+            out["workloads"] = json.load(f).get("workloads", {})
+        specs = specs[2:]
     for spec in specs:
         d, workload, units = spec.rsplit(":", 2)
         units = float(units)
