@@ -71,6 +71,7 @@ SIGNATURES = {
     "bbm_hip_scratch_trim": (_SZ, []),
     "bbm_hip_scratch_trim_captured": (_SZ, []),
     "bbm_hip_scratch_bytes": (_SZ, []),
+    "bbm_hip_libm_eval": (_I, [_I, _P, _P, _P, _SZ, _P]),
 }
 
 ABI_VERSION = 10

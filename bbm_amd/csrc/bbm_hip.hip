@@ -554,6 +554,26 @@ __global__ __launch_bounds__(kBlock) void k_sphere_dirs(const float* u0, const f
   }
 }
 
+// bbm_hip_libm_eval: the device's restated libm floats, elementwise
+__global__ __launch_bounds__(kBlock) void k_libm(int func, const float* a, const float* b, float* out, uint64_t n)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
+  {
+    const float x = a[i];
+    float r;
+    switch (func)
+    {
+      case BBM_HIP_LIBM_EXPF: r = expf_glibc(x); break;
+      case BBM_HIP_LIBM_LOGF: r = logf_glibc(x); break;
+      case BBM_HIP_LIBM_POWF: r = powf_glibc(x, b[i]); break;
+      case BBM_HIP_LIBM_ERFF: r = erff_glibc(x); break;
+      default: r = erfcf_glibc(x); break;
+    }
+    out[i] = r;
+  }
+}
+
 int launched()
 {
   const hipError_t e = hipGetLastError();
@@ -1039,6 +1059,18 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
   hipLaunchKernelGGL(k_sphere_dirs, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), xi0, xi1,
                      uint64_t(n), hemisphere, x, y, z);
+  return launched();
+}
+
+int bbm_hip_libm_eval(int func, const float* a, const float* b, float* out, size_t n, void* stream)
+{
+  if (n == 0) return BBM_HIP_OK;
+  if (func < BBM_HIP_LIBM_EXPF || func > BBM_HIP_LIBM_ERFCF) return fail(BBM_HIP_ERR_INVALID_ARG, "unknown libm function");
+  if (!a || !out || (func == BBM_HIP_LIBM_POWF && !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "pointer is NULL");
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipLaunchKernelGGL(k_libm, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), func, a, b, out,
+                     uint64_t(n));
   return launched();
 }
 

@@ -176,9 +176,11 @@ struct He
     const float cot = div_nr(1.0f, tan_theta(v));
     // the double quotients below are stored straight into floats: f_div_d rounds like the reference
     const float scot = f_div_d(double(tau * cot), 2.0 * double(sigma0));
-    const float erfc_ = 0.5f * erfcf(scot);   // float(0.5 * double(e)): exact
+    const float erfc_ = 0.5f * erfcf_glibc(scot);   // float(0.5 * double(e)): exact; glibc's erfcf, bit for bit
     float lambda = f_div_d(0.5 * double(kInvSqrtPiF), double(scot));
-    if (ERRATA) lambda = float(double(lambda) * double(exp_d2f(-(double(scot) * double(scot)))));
+    // Lambda *= exp(-pow(scot, 2.0)): a float times the double exponential, rounded once (compound assignment of a
+    // double to a float); exp_dd is within ~2^-44 of glibc's exp, so the product rounds like the reference's
+    if (ERRATA) lambda = float(double(lambda) * exp_dd(fmax(-(double(scot) * double(scot)), -745.0)));
     lambda -= erfc_;
     const float S = f_div_d(1.0 - double(erfc_), double(lambda) + 1.0);
     return smooth ? 1.0f : S;
@@ -209,7 +211,7 @@ struct He
   __device__ __forceinline__ float sigma(v3 in, v3 out) const
   {
     const float ti = tan_theta(in), to = tan_theta(out);
-    auto K = [&](float t) { return t * erfcf(div_nr(tau, 2 * sigma0 * t)); };
+    auto K = [&](float t) { return t * erfcf_glibc(div_nr(tau, 2 * sigma0 * t)); };
     const float Ki = (ti > kEpsF) ? K(ti) : 0.0f;
     const float Ko = (to > kEpsF) ? K(to) : 0.0f;
     const float f0 = div_nr(1.0f, sqrtf(kPi8F)) * (Ki + Ko);
@@ -219,7 +221,10 @@ struct He
 #pragma unroll
     for (int s = 0; s < 4; ++s)
     {
-      const float expn = exp_d2f(0.5 * double(x) * double(x));
+      // Value expn = exp(0.5 * x * x): the double exponential rounded to float -- exp2_cr (correctly rounded but
+      // within ~2^-18 ulp of a midpoint), as glibc's 0.51-ulp exp rounded to float; exp_d2f's 1.5 ulp moved the
+      // Newton root by an ulp on ~10 % of the lanes
+      const float expn = exp2_cr(0.5 * double(x) * double(x) * 1.4426950408889634074);
       const float ev = x * expn - f0;
       const float grad = (1 + x * x) * expn;
       x -= (grad > kEpsF) ? div_nr(ev, grad) : 0.0f;

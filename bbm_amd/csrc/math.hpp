@@ -392,6 +392,118 @@ __device__ __forceinline__ float powf_glibc(float x, float y)
   return (y == 0.0f || x == 1.0f) ? 1.0f : res;
 }
 
+// glibc 2.35's erff / erfcf (sysdeps/ieee754/flt-32/s_erff.c: Sun fdlibm's rational approximations in float
+// arithmetic, no FMA variant, __ieee754_expf = the expf above), restated op for op -- what the reference's
+// bbm::erf / bbm::erfc of a float return (std::erf / std::erfc -> erff / erfcf).  Neither is correctly rounded; the
+// He family's shadowing term S1 subtracts erfc from a nearly equal quantity and the Beckmann VNDF sampler inverts
+// erf by Newton steps, so only glibc's own floats reproduce the reference there.  Coefficients: fdlibm's floats as
+// this machine's libm.so.6 holds them.  Pinned on all 2^32 inputs by oracle/erfcf_glibc_check.c (0 mismatches).
+namespace fdlibm_erf {
+constexpr float erx = 8.4506291151e-01f, pp0 = 1.2837916613e-01f, pp1 = -3.2504209876e-01f,
+                pp2 = -2.8481749818e-02f, pp3 = -5.7702702470e-03f, pp4 = -2.3763017452e-05f, qq1 = 3.9791721106e-01f,
+                qq2 = 6.5022252500e-02f, qq3 = 5.0813062117e-03f, qq4 = 1.3249473704e-04f, qq5 = -3.9602282413e-06f,
+                pa0 = -2.3621185683e-03f, pa1 = 4.1485610604e-01f, pa2 = -3.7220788002e-01f, pa3 = 3.1834661961e-01f,
+                pa4 = -1.1089469492e-01f, pa5 = 3.5478305072e-02f, pa6 = -2.1663755178e-03f, qa1 = 1.0642088205e-01f,
+                qa2 = 5.4039794207e-01f, qa3 = 7.1828655899e-02f, qa4 = 1.2617121637e-01f, qa5 = 1.3637083583e-02f,
+                qa6 = 1.1984500103e-02f, ra0 = -9.8649440333e-03f, ra1 = -6.9385856390e-01f, ra2 = -1.0558626175e+01f,
+                ra3 = -6.2375331879e+01f, ra4 = -1.6239666748e+02f, ra5 = -1.8460508728e+02f, ra6 = -8.1287437439e+01f,
+                ra7 = -9.8143291473e+00f, sa1 = 1.9651271820e+01f, sa2 = 1.3765776062e+02f, sa3 = 4.3456588745e+02f,
+                sa4 = 6.4538726807e+02f, sa5 = 4.2900814819e+02f, sa6 = 1.0863500214e+02f, sa7 = 6.5702495575e+00f,
+                sa8 = -6.0424413532e-02f, rb0 = -9.8649431020e-03f, rb1 = -7.9928326607e-01f, rb2 = -1.7757955551e+01f,
+                rb3 = -1.6063638306e+02f, rb4 = -6.3756646729e+02f, rb5 = -1.0250950928e+03f, rb6 = -4.8351919556e+02f,
+                sb1 = 3.0338060379e+01f, sb2 = 3.2579251099e+02f, sb3 = 1.5367296143e+03f, sb4 = 3.1998581543e+03f,
+                sb5 = 2.5530502930e+03f, sb6 = 4.7452853394e+02f, sb7 = -2.2440952301e+01f;
+
+// |x| < 0.84375: y = r / s of the erf expansion in z = x^2
+__device__ __forceinline__ float small_y(float x)
+{
+  const float z = x * x;
+  const float r = pp0 + z * (pp1 + z * (pp2 + z * (pp3 + z * pp4)));
+  const float s = 1.0f + z * (qq1 + z * (qq2 + z * (qq3 + z * (qq4 + z * qq5))));
+  return div_nr(r, s);
+}
+// 0.84375 <= |x| < 1.25: P / Q in s = |x| - 1
+__device__ __forceinline__ float mid_pq(float ax)
+{
+  const float s = ax - 1.0f;
+  const float P = pa0 + s * (pa1 + s * (pa2 + s * (pa3 + s * (pa4 + s * (pa5 + s * pa6)))));
+  const float Q = 1.0f + s * (qa1 + s * (qa2 + s * (qa3 + s * (qa4 + s * (qa5 + s * qa6)))));
+  return div_nr(P, Q);
+}
+// 1.25 <= |x| < 28: erfc(|x|) |x| = exp(-z^2 - 0.5625) exp((z - |x|)(z + |x|) + R/S), z = |x| with the low mantissa
+// bits cleared (`mask`), R/S in s = 1/x^2 on [1.25, 1/0.35) or beyond (`split`).  The second branch's polynomials
+// have one coefficient fewer: a zero top coefficient leaves every rounding unchanged (c + s 0 = c), so one Horner
+// chain with selected coefficients serves both.
+__device__ __forceinline__ float tail_r(float ax, uint32_t split, uint32_t mask)
+{
+  const bool a = __float_as_uint(ax) < split;
+  const float s = div_nr(1.0f, ax * ax);
+  const float R = (a ? ra0 : rb0) + s * ((a ? ra1 : rb1) + s * ((a ? ra2 : rb2) + s * ((a ? ra3 : rb3) +
+                  s * ((a ? ra4 : rb4) + s * ((a ? ra5 : rb5) + s * ((a ? ra6 : rb6) + s * (a ? ra7 : 0.0f)))))));
+  const float S = 1.0f + s * ((a ? sa1 : sb1) + s * ((a ? sa2 : sb2) + s * ((a ? sa3 : sb3) + s * ((a ? sa4 : sb4) +
+                  s * ((a ? sa5 : sb5) + s * ((a ? sa6 : sb6) + s * ((a ? sa7 : sb7) + s * (a ? sa8 : 0.0f))))))));
+  const float z = __uint_as_float(__float_as_uint(ax) & mask);
+  return expf_glibc(-z * z - 0.5625f) * expf_glibc((z - ax) * (z + ax) + div_nr(R, S));
+}
+}  // namespace fdlibm_erf
+
+__device__ __forceinline__ float erfcf_glibc(float x)
+{
+  using namespace fdlibm_erf;
+  const uint32_t hx = __float_as_uint(x), ix = hx & 0x7fffffffu;
+  const bool neg = (hx >> 31) != 0;
+  const float ax = __builtin_fabsf(x);
+  float res;
+  if (ix < 0x3f580000u)
+  {
+    const float y = small_y(x);
+    float r = x * y;
+    r += (x - 0.5f);
+    res = (int32_t(hx) < 0x3e800000) ? 1.0f - (x + x * y) : 0.5f - r;
+    res = (ix < 0x32800000u) ? 1.0f - x : res;
+  }
+  else if (ix < 0x3fa00000u)
+  {
+    const float pq = mid_pq(ax);
+    res = neg ? 1.0f + (erx + pq) : (1.0f - erx) - pq;
+  }
+  else if (ix < 0x41e00000u)
+  {
+    // r / x can fall to ~1e-37 (x ~ 9): the f64 remainder step (div_sub<true>) keeps that quotient exact where
+    // div_nr's f32 remainder would be subnormal
+    const float q = div_sub<true>(tail_r(ax, 0x4036DB6Du, 0xffffe000u), ax);
+    res = neg ? ((ix >= 0x40c00000u) ? 2.0f : 2.0f - q) : q;    // x < -6: 2 - tiny = 2
+  }
+  else res = neg ? 2.0f : 0.0f;                                // |x| >= 28 (inf included): 2 - tiny, tiny^2
+  return (x != x) ? x : res;
+}
+
+__device__ __forceinline__ float erff_glibc(float x)
+{
+  using namespace fdlibm_erf;
+  const uint32_t hx = __float_as_uint(x), ix = hx & 0x7fffffffu;
+  const bool neg = (hx >> 31) != 0;
+  const float ax = __builtin_fabsf(x);
+  float res;
+  if (ix < 0x3f580000u)
+  {
+    res = x + x * small_y(x);
+    res = (ix < 0x31800000u) ? ((ix < 0x04000000u) ? 0.0625f * (16.0f * x + (16.0f * pp0) * x) : x + pp0 * x) : res;
+  }
+  else if (ix < 0x3fa00000u)
+  {
+    const float pq = mid_pq(ax);
+    res = neg ? -erx - pq : erx + pq;
+  }
+  else if (ix < 0x40c00000u)
+  {
+    const float q = div_sub<true>(tail_r(ax, 0x4036DB6Eu, 0xfffff000u), ax);
+    res = neg ? q - 1.0f : 1.0f - q;
+  }
+  else res = neg ? -1.0f : 1.0f;                               // |x| >= 6 (inf included): +-(1 - tiny)
+  return (x != x) ? x : res;
+}
+
 // a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
 // q = a rm corrected once by the exact remainder -- the correctly rounded quotient (as div_nr) without v_rcp_f32
 __device__ __forceinline__ float div_small(float a, float m, float rm)

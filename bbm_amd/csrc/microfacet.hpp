@@ -70,15 +70,17 @@ struct Beckmann
     if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
     const v3 vs = normalize3(mk3(view.x * au, view.y * av, view.z));
     const float tanT = tan_theta(vs);
-    const float maxval = erff(div_nr(1.0f, tanT));
+    // erf, log and exp of floats: glibc's erff / logf / expf restated bit for bit (math.hpp), so the Newton
+    // iteration starts from and converges to the reference's own floats
+    const float maxval = erff_glibc(div_nr(1.0f, tanT));
     float xc0 = clampf(xi0, float(10e-6), float(1.0 - 10e-6));
     const float xc1 = clampf(xi1, float(10e-6), float(1.0 - 10e-6));
-    float x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
-    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_dn(-(vs.z * vs.z))));
+    float x = maxval - (maxval + 1) * erff_glibc(sqrtf(-logf_glibc(xc0)));
+    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_glibc_neg(-(vs.z * vs.z))));
     for (int i = 0; i < 3; ++i)
     {
       const float slope = erfinv_s(x);
-      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_dn(-slope * slope) - xc0);
+      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_glibc_neg(-slope * slope) - xc0);
       // float(1.0 - p) of a float p: one double op on float operands rounded to float is the float op itself
       // (53 >= 2 x 24 + 2), so the f32 subtraction -- likewise 2 xc1 - 1 below (2 xc1 exact in either type)
       const float der = 1.0f - slope * tanT;

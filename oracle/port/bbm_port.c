@@ -419,3 +419,20 @@ int bbmport_sample(const char* name, const float* params, int nparams, size_t n,
   }
   return 0;
 }
+
+int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n)
+{
+  for (size_t i = 0; i < n; ++i)
+  {
+    switch (func)
+    {
+      case 0: out[i] = expf(a[i]); break;
+      case 1: out[i] = logf(a[i]); break;
+      case 2: out[i] = powf(a[i], b[i]); break;
+      case 3: out[i] = erff(a[i]); break;
+      case 4: out[i] = erfcf(a[i]); break;
+      default: return -1;
+    }
+  }
+  return 0;
+}

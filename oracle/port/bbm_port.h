@@ -33,6 +33,10 @@ int bbmport_sample(const char* name, const float* params, int nparams, size_t n,
                    const float* xi0, const float* xi1, uint32_t component, uint32_t unit,
                    float* dx, float* dy, float* dz, float* pdf, uint32_t* flag, int nthreads);
 
+/* the host libm float functions elementwise (0 expf, 1 logf, 2 powf(a, b), 3 erff, 4 erfcf): what the reference's
+ * native backbone calls, for pinning the device restatements (bbm_hip_libm_eval) on the same machine */
+int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

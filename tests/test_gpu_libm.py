@@ -1,0 +1,83 @@
+"""The device restatements of the host libm float functions the reference's native backbone calls (math.hpp:
+expf_glibc, logf_glibc, powf_glibc, erff_glibc, erfcf_glibc) against the host libm of the machine running the test,
+through bbm_hip_libm_eval: bit-identical floats (NaN = NaN) on strided sweeps of every float bit pattern and on
+random (x, y) pairs for powf.  The C restatements of the same steps are pinned exhaustively on the CPU
+(tests/test_oracle.py, oracle/*_check.c); this pins the device code to them."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests import oracle_util as ou
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import bbm_amd
+    from bbm_amd import _lib
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    torch.cuda.set_device(0)
+    return _lib.load()
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _device(lib, func, a, b=None):
+    from bbm_amd import _lib
+    da = torch.from_numpy(a).cuda()
+    db = torch.from_numpy(b).cuda() if b is not None else None
+    out = torch.empty_like(da)
+    _lib.check(lib.bbm_hip_libm_eval(FUNCS[func], da.data_ptr(), db.data_ptr() if db is not None else None,
+                                     out.data_ptr(), a.size, None))
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _host(func, a, b=None):
+    out = np.empty_like(a)
+    rc = ou.port().bbmport_libm(FUNCS[func], _fp(a), _fp(b) if b is not None else None, _fp(out),
+                                ctypes.c_size_t(a.size))
+    assert rc == 0
+    return out
+
+
+def _same(got, want):
+    g, w = got.view(np.uint32), want.view(np.uint32)
+    return (g == w) | (np.isnan(got) & np.isnan(want))
+
+
+def _sweep(stride, offset=0):
+    return (np.arange(offset, 1 << 32, stride, dtype=np.uint64)).astype(np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("func", ["expf", "logf", "erff", "erfcf"])
+def test_unary_bitexact_sweep(lib, func):
+    a = _sweep(251, 7)            # 17.1 M bit patterns: both signs, subnormals, inf, NaN
+    got, want = _device(lib, func, a), _host(func, a)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"{func}: {bad.size} lanes differ, e.g. x={a[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"
+
+
+def test_powf_bitexact(lib):
+    rng = np.random.default_rng(20261017)
+    n = 1 << 22
+    xs = [rng.integers(0, 0x7f800000, n, dtype=np.uint32).view(np.float32),       # any positive float
+          rng.uniform(0, 4, n).astype(np.float32),                                  # Bagher (theta - theta0, k), (t, p)
+          rng.uniform(0, 4, n).astype(np.float32),
+          rng.integers(0, 0x00800000, n, dtype=np.uint32).view(np.float32)]         # subnormal x
+    ys = [rng.uniform(-64, 64, n).astype(np.float32), rng.uniform(0, 64, n).astype(np.float32),
+          rng.uniform(0, 2, n).astype(np.float32), rng.uniform(-2, 2, n).astype(np.float32)]
+    specials = np.array([0, 0, 1, 1, np.inf, np.inf, np.nan, 2, 0.5], np.float32)
+    specials_y = np.array([2, -2, 7.5, np.nan, 3, -3, 0, 0, np.inf], np.float32)
+    a = np.concatenate(xs + [specials])
+    b = np.concatenate(ys + [specials_y])
+    got, want = _device(lib, "powf", a, b), _host("powf", a, b)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"powf: {bad.size} lanes differ, e.g. x={a[bad[:4]]} y={b[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"

@@ -154,3 +154,32 @@ def test_expf_restatement_matches_host_libm():
     r = subprocess.run([exe, "61"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout
     assert " 0 mismatches" in r.stdout
+
+
+def _run_check(name, *args):
+    import os
+    import subprocess
+    exe = os.path.join(ou.ROOT, "oracle", "_port", name)
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ou.ROOT, "oracle"), "expf"], check=True, capture_output=True)
+    r = subprocess.run([exe] + [str(a) for a in args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout
+    return r.stdout
+
+
+def test_powf_logf_restatements_match_host_libm():
+    """math.hpp powf_glibc / logf_glibc restate glibc's powf / logf (the reference's bbm::pow / bbm::log of floats);
+    oracle/glibcf_check runs the same double steps in C against this host's libm: logf on every positive float, powf
+    on 5 x 4e6 random pairs here (the full run, 1e9 pairs, 0 mismatches -- DESIGN.md §4.2).  It also counts how often
+    glibc's powf is not the correctly rounded float -- the reason the restatement must be glibc's, not the nearest."""
+    out = _run_check("glibcf_check", 4000000)
+    assert "logf: 2139095039 positive floats, 0 mismatches" in out, out
+    assert "powf: 20000000 (x, y) pairs, 0 mismatches" in out, out
+
+
+def test_erff_erfcf_restatements_match_host_libm():
+    """math.hpp erff_glibc / erfcf_glibc restate glibc's float erf / erfc (fdlibm's s_erff.c); oracle/erfcf_glibc_check
+    compares the C restatement with this host's libm on every 31st float bit pattern here (stride 1: all 2^32, 0
+    mismatches)."""
+    out = _run_check("erfcf_glibc_check", 31)
+    assert "erfcf 0 mismatches, erff 0 mismatches" in out, out
