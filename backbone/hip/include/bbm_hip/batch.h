@@ -381,7 +381,9 @@ namespace bbm {
       int id = -1;
       std::vector<T> params;
       std::vector<basic_model_desc> kids;
-      bool composed(void) const { return id == BBM_HIP_AGGREGATE; }
+      //! a composed aggregate: the template type's aggregatemodel (BBM_HIP_AGGREGATE) or, from a string / bsdf_ptr,
+      //! the runtime aggregatebsdf (BBM_HIP_AGGREGATE_BSDF; a fused one carries BBM_HIP_RUNTIME_AGGREGATE in its id)
+      bool composed(void) const { return id == BBM_HIP_AGGREGATE || id == BBM_HIP_AGGREGATE_BSDF; }
     };
     using model_desc = basic_model_desc<float>;
     using model_desc_f64 = basic_model_desc<double>;
@@ -404,6 +406,13 @@ namespace bbm {
           store.reserve(64);
           root = build(m);
           count = int(m.kids.size());
+          if(m.id == BBM_HIP_AGGREGATE_BSDF)
+          {
+            // the runtime aggregate's own semantics at the top level: passed as its root node (include/bbm_hip.h)
+            store.push_back(std::vector<child_t>{child_t{BBM_HIP_AGGREGATE_BSDF, nullptr, 0, root, count}});
+            root = store.back().data();
+            count = 1;
+          }
         }
         const child_t* build(const basic_model_desc<T>& m)
         {
@@ -411,7 +420,7 @@ namespace bbm {
           for(size_t k = 0; k < m.kids.size(); ++k)
           {
             const auto& c = m.kids[k];
-            if(c.composed()) v[k] = child_t{BBM_HIP_AGGREGATE, nullptr, 0, build(c), int(c.kids.size())};
+            if(c.composed()) v[k] = child_t{c.id, nullptr, 0, build(c), int(c.kids.size())};
             else v[k] = child_t{c.id, c.params.data(), int(c.params.size()), nullptr, 0};
           }
           if(store.size() == store.capacity()) throw error(BBM_HIP_ERR_INVALID_ARG, "aggregate tree too large");
@@ -511,11 +520,36 @@ namespace bbm {
       return describe_as<float>(model);
     }
 
+    namespace detail {
+      //! the template type's semantics all the way down: aggregatemodel nodes and plain fused ids
+      template<typename T>
+        inline void as_template(basic_model_desc<T>& d)
+      {
+        if(d.id == BBM_HIP_AGGREGATE_BSDF) d.id = BBM_HIP_AGGREGATE;
+        else if(d.id >= 0) d.id &= ~BBM_HIP_RUNTIME_AGGREGATE;
+        for(auto& k : d.kids) as_template(k);
+      }
+    } // end detail namespace
+
 #ifdef _BBM_BSDF_PTR_H_
     //! \brief bsdf_ptr<C> (include/bbm/bsdf_ptr.h:21-165): through its toString (bsdf.h:111-116 pipes the
-    //! wrapped model's) and the library's parser
+    //! wrapped model's) and the library's parser.  The string of a bsdf<aggregatemodel<...>> and of the runtime
+    //! aggregatebsdf (aggregatebsdf.h:40-190, what fromString<bsdf_ptr> builds) read alike, but they round the
+    //! pdf differently and sample differently: the wrapped object decides -- an aggregatebsdf keeps the parser's
+    //! runtime semantics (its children are the bsdf_ptrs its string describes), anything else is a template
+    //! model, aggregatemodel at every level.
     template<typename C>
-      inline model_desc describe(const bbm::bsdf_ptr<C>& ptr) { return from_string(ptr.toString()); }
+      inline model_desc describe(const bbm::bsdf_ptr<C>& ptr)
+    {
+      model_desc d = from_string(ptr.toString());
+#ifdef _BBM_AGGREGATEBSDF_H_
+      const bool runtime = dynamic_cast<const bbm::aggregatebsdf<C>*>(ptr.ptr().get()) != nullptr;
+#else
+      const bool runtime = false;      // aggregatebsdf.h not included: no runtime aggregate can exist
+#endif
+      if(!runtime) detail::as_template(d);
+      return d;
+    }
 #endif
 
     //! \brief libbbm_hip model id of MODEL's single kernel (resolved once per type)

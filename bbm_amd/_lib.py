@@ -76,6 +76,8 @@ SIGNATURES = {
 
 ABI_VERSION = 10
 AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
+AGGREGATE_BSDF = -101   # BBM_HIP_AGGREGATE_BSDF: a composed runtime aggregate (aggregatebsdf, what fromString builds)
+RUNTIME_AGGREGATE = 0x40000000   # BBM_HIP_RUNTIME_AGGREGATE: OR-ed into a fused aggregate's id -> aggregatebsdf semantics
 
 
 class Child(ctypes.Structure):

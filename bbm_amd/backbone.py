@@ -180,6 +180,13 @@ class BsdfModel:
         for k, v in values.items():
             self.set_attribute(k, v)
 
+    @property
+    def runtime(self):
+        """A fused Aggregate(A, B) evaluated as the reference's runtime aggregatebsdf (what fromString / bsdf_import
+        build, include/bbm/aggregatebsdf.h) rather than as aggregatemodel<A, B>: the model id carries
+        BBM_HIP_RUNTIME_AGGREGATE."""
+        return self.model_id >= 0 and bool(self.model_id & _lib.RUNTIME_AGGREGATE)
+
     # ---------------------------------------------------------------- attributes
     def _slot(self, attr):
         k = 0
@@ -441,7 +448,8 @@ def _parse_model(tok, i, s):
             kids.append(m)
             if tok[i] == ",":
                 i += 1
-        return Aggregate(*kids), i + 1
+        # the runtime aggregate: fromString<bsdf_ptr> maps "Aggregate" to aggregatebsdf (bsdf_string_convert.h:59)
+        return Aggregate(*kids, runtime=True), i + 1
     if name not in ATTRIBUTES:
         raise ValueError(f"unknown BSDF model: {name}")
     m = BsdfModel(name)
@@ -486,7 +494,7 @@ def _copy_model(m):
     class, own parameter vector, and every other attribute shared -- a Merl child keeps the reference to the
     device table its parameters point to."""
     if isinstance(m, AggregateModel):
-        return AggregateModel(*m._children)
+        return AggregateModel(*m._children, runtime=m.runtime)
     c = copy.copy(m)
     c._params = m._params.copy()
     return c
@@ -502,7 +510,7 @@ class AggregateModel:
     picks them).  Parameters are the children's vectors in order (reflection order of the base classes).
     float32 tensors evaluate in floatRGB, float64 tensors in doubleRGB (every leaf needs doubleRGB kernels)."""
 
-    def __init__(self, *children):
+    def __init__(self, *children, runtime=False):
         if len(children) < 2:
             raise ValueError("an aggregate needs at least two child models")
         for c in children:
@@ -510,6 +518,9 @@ class AggregateModel:
                 raise TypeError("aggregate children must be models (BsdfModel, Merl or AggregateModel)")
         self._children = [_copy_model(c) for c in children]
         self.name = aggregate_key([c.name for c in children])
+        # runtime: the reference's aggregatebsdf (left folds, per-term pdf quotients, no sample unless the weights
+        # sum to > eps; include/bbm/aggregatebsdf.h), what fromString builds; else aggregatemodel<...>
+        self.runtime = bool(runtime)
 
     def children(self):
         return [_copy_model(c) for c in self._children]
@@ -535,28 +546,48 @@ class AggregateModel:
     def has_f64(self):
         return all(c.has_f64() for c in self._children)
 
-    def _desc(self, f64=False):
-        """ctypes bbm_hip_child(_f64) array of the children, nested aggregates as AGGREGATE nodes; returns (array,
-        keep-alive list of the arrays and parameter buffers it points to)."""
+    def _desc(self, f64=False, params=None):
+        """ctypes bbm_hip_child(_f64) tree: (array, count, keep-alive list of the arrays and parameter buffers it
+        points to).  An aggregatemodel passes its children (count >= 2); a runtime aggregate passes its root node
+        (count 1, BBM_HIP_AGGREGATE_BSDF), the only way to give the top level aggregatebsdf semantics.  Nested
+        aggregates are AGGREGATE / AGGREGATE_BSDF nodes.  params: the flat parameter vector to use instead of the
+        children's own (the leaves in preorder)."""
         keep = []
         kind = _lib.ChildF64 if f64 else _lib.Child
+        flat = None if params is None else np.asarray(params).reshape(-1)
+        off = [0]
+
+        def leaf_params(c):
+            if flat is None:
+                return c._params
+            k = c._params.size
+            off[0] += k
+            return flat[off[0] - k:off[0]]
+
+        def node(a, c):
+            if isinstance(c, AggregateModel):
+                sub = build(c._children)
+                a.model_id, a.params, a.nparams = (_lib.AGGREGATE_BSDF if c.runtime else _lib.AGGREGATE), None, 0
+                a.children, a.nchildren = ctypes.cast(sub, ctypes.c_void_p), len(c._children)
+            else:
+                c._pptr()          # a Merl child checks its table's device here
+                p = np.ascontiguousarray(leaf_params(c), dtype=np.float64 if f64 else np.float32)
+                keep.append(p)
+                a.model_id, a.params, a.nparams = c.model_id, p.ctypes.data, p.size
+                a.children, a.nchildren = None, 0
 
         def build(kids):
             arr = (kind * len(kids))()
             keep.append(arr)
             for a, c in zip(arr, kids):
-                if isinstance(c, AggregateModel):
-                    sub = build(c._children)
-                    a.model_id, a.params, a.nparams = _lib.AGGREGATE, None, 0
-                    a.children, a.nchildren = ctypes.cast(sub, ctypes.c_void_p), len(c._children)
-                else:
-                    c._pptr()          # a Merl child checks its table's device here
-                    p = np.ascontiguousarray(c._params, dtype=np.float64) if f64 else c._params
-                    keep.append(p)
-                    a.model_id, a.params, a.nparams = c.model_id, p.ctypes.data, p.size
-                    a.children, a.nchildren = None, 0
+                node(a, c)
             return arr
-        return build(self._children), keep
+        if self.runtime:
+            root = (kind * 1)()
+            keep.append(root)
+            node(root[0], self)
+            return root, 1, keep
+        return build(self._children), len(self._children), keep
 
     def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
                  rgb=None, pdf=None, stream=None, mode=3):
@@ -572,9 +603,9 @@ class AggregateModel:
         if mode & 2:
             pdf = torch.empty((n,), dtype=dt, device=dev) if pdf is None else _out_rows(pdf, 0, n, dev, "pdf", dt)
         _on_stream(stream, _keep, rgb, pdf)
-        d, _kd = self._desc(f64)
+        d, nd, _kd = self._desc(f64)
         fn = _lib.load().bbm_hip_aggregate_eval_pdf_f64 if f64 else _lib.load().bbm_hip_aggregate_eval_pdf
-        _lib.check(fn(d, len(self._children), ix, iy, iz, ox, oy, oz, mptr, n, int(component), int(unit),
+        _lib.check(fn(d, nd, ix, iy, iz, ox, oy, oz, mptr, n, int(component), int(unit),
                       rgb[0].data_ptr() if mode & 1 else None, rgb[1].data_ptr() if mode & 1 else None,
                       rgb[2].data_ptr() if mode & 1 else None, pdf.data_ptr() if mode & 2 else None,
                       _stream_ptr(stream)))
@@ -598,9 +629,9 @@ class AggregateModel:
         p = torch.empty((n,), dtype=dt, device=dev)
         f = torch.empty((n,), dtype=torch.int32, device=dev)
         _on_stream(stream, _keep, d, p, f)
-        desc, _kd = self._desc(f64)
+        desc, nd, _kd = self._desc(f64)
         fn = _lib.load().bbm_hip_aggregate_sample_f64 if f64 else _lib.load().bbm_hip_aggregate_sample
-        _lib.check(fn(desc, len(self._children), ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
+        _lib.check(fn(desc, nd, ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
                       int(unit), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
                       _stream_ptr(stream)))
         return BsdfSample(d, p, f)
@@ -614,21 +645,26 @@ class AggregateModel:
         dev = (out[0] if isinstance(out, (tuple, list)) else out).device
         rgb = torch.empty((3, n), dtype=dt, device=dev)
         _on_stream(stream, _keep, rgb)
-        desc, _kd = self._desc(f64)
+        desc, nd, _kd = self._desc(f64)
         fn = _lib.load().bbm_hip_aggregate_reflectance_f64 if f64 else _lib.load().bbm_hip_aggregate_reflectance
-        _lib.check(fn(desc, len(self._children), ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
+        _lib.check(fn(desc, nd, ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
                       rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
         return rgb
 
 
-def Aggregate(*children, fused=True):
+def Aggregate(*children, fused=True, runtime=False):
     """aggregate(models...) (aggregatemodel.h:232-233): the fused kernel for the published fits' form
     Aggregate(Lambertian, X) where one is registered (fused=False forces the composed path), otherwise an
-    AggregateModel over the children's own kernels."""
+    AggregateModel over the children's own kernels.  runtime=True: the reference's runtime aggregatebsdf
+    (aggregatebsdf.h, the aggregate of bsdf_ptrs that fromString / bsdf_import / checkBsdf build) instead of
+    aggregatemodel<...> -- same eval for two children, but the pdf's and sample's own rounding and rules."""
     key = aggregate_key([c.name for c in children])
     if fused and key in AGGREGATES and all(isinstance(c, BsdfModel) for c in children):
-        return BsdfModel(key, *children)
-    return AggregateModel(*children)
+        m = BsdfModel(key, *children)
+        if runtime:
+            m.model_id |= _lib.RUNTIME_AGGREGATE
+        return m
+    return AggregateModel(*children, runtime=runtime)
 
 
 def _make_ctor(name):

@@ -5,20 +5,34 @@
 //   pdf         = (w_A pdf_A + w_B pdf_B) / (w_A + w_B), w = hsum(reflectance(out)), 0 if sum <= eps (:129-143)
 //   sample      = pick A or B by xi0 * sum against w_A, rescale xi0, sample it; pdf as above (:81-113)
 //   reflectance = A.reflectance + B.reflectance                              (:156-163)
+//
+// The same two children as the RUNTIME aggregate bsdf_import / fromString<bsdf_ptr> builds (aggregatebsdf,
+// include/bbm/aggregatebsdf.h:40-190; bsdf_string_convert.h:59 maps "Aggregate" to it): eval and reflectance are
+// left folds from 0 -- for two children the same floats -- but
+//   pdf    = w_A pdf_A / sum + w_B pdf_B / sum, one quotient per term, 0 unless sum > eps (:173-187)
+//   sample = no sample at all unless sum > eps (:113-116: the reference returns a default-constructed, i.e.
+//            indeterminate, BsdfSample there; this returns {0, 0, None}); otherwise the same child selection, and
+//            the pdf at the sampled direction term by term as above (:133-137)
+// Selected per launch by the parameter block's last slot (kAggregateModeSlot, set by the C-ABI for model ids
+// carrying BBM_HIP_RUNTIME_AGGREGATE); 0 (every other path) is aggregatemodel.
 #pragma once
 #include "math.hpp"
 #include "microfacet.hpp"
 
 namespace bbmhip {
 
+constexpr int kAggregateModeSlot = 63;     // ParamBlock slot (kernels.hpp kMaxParams - 1): 1 = aggregatebsdf semantics
+
 template<class A, class B>
 struct Aggregate
 {
   static constexpr int kParams = A::kParams + B::kParams;
   static constexpr uint32_t kComponent = A::kComponent | B::kComponent;
+  static_assert(kParams + 3 <= kAggregateModeSlot, "the mode slot must lie beyond the children's parameter blocks");
   A a;
   B b;
-  __device__ explicit Aggregate(const float* p) : a(p), b(p + A::kParams) {}
+  bool runtime;            // aggregatebsdf (fromString / bsdf_ptr) rather than aggregatemodel semantics
+  __device__ explicit Aggregate(const float* p) : a(p), b(p + A::kParams), runtime(p[kAggregateModeSlot] != 0.0f) {}
 
   // hsum(reflectance(out)) per child: std::accumulate from Value(0) (horizontal.h:64-67)
   __device__ __forceinline__ void weights(v3 out, uint32_t component, float& wa, float& wb) const
@@ -30,12 +44,14 @@ struct Aggregate
     wb = ((0.0f + rb[0]) + rb[1]) + rb[2];
   }
 
-  // inner_product(pdfs, weights, Value(0)) / sum, masked sum > eps (:141-142)
-  __device__ __forceinline__ static float mix(float pa, float pb, float wa, float wb)
+  // aggregatemodel: inner_product(pdfs, weights, Value(0)) / sum, masked sum > eps (:141-142); aggregatebsdf:
+  // pdf += weight * pdf_k / sum per child from 0 (aggregatebsdf.h:183-187)
+  __device__ __forceinline__ float mix(float pa, float pb, float wa, float wb) const
   {
     const float sum = (0.0f + wa) + wb;
     const float ip = (0.0f + pa * wa) + pb * wb;
-    return (sum > kEpsF) ? div_nr(ip, sum) : 0.0f;
+    const float tm = (0.0f + div_nr(wa * pa, sum)) + div_nr(wb * pb, sum);
+    return (sum > kEpsF) ? (runtime ? tm : div_nr(ip, sum)) : 0.0f;
   }
 
   template<int MODE>
@@ -76,6 +92,7 @@ struct Aggregate
     float wa, wb;
     weights(out, component, wa, wb);
     const float sum = (0.0f + wa) + wb;
+    if (runtime && !(sum > kEpsF)) return;        // aggregatebsdf's bail-out (:115-116)
     float x = xi0 * sum;
     // CONSTFOREACH over the children in order; a later child that also claims x overrides (:95-108)
     const bool ma = (x >= 0) && (x <= wa);

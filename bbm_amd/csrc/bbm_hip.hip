@@ -395,7 +395,17 @@ const Registry& registry()
 }
 
 int num_models() { return int(registry().models.size()); }
-const ModelEntry* entry(int id) { return (id >= 0 && id < num_models()) ? &registry().models[size_t(id)] : nullptr; }
+// a registry id, or a fused aggregate's id with BBM_HIP_RUNTIME_AGGREGATE (its aggregatebsdf semantics)
+bool runtime_id(int id) { return id >= 0 && (id & BBM_HIP_RUNTIME_AGGREGATE) != 0; }
+const ModelEntry* entry(int id)
+{
+  const int base = (id >= 0) ? (id & ~BBM_HIP_RUNTIME_AGGREGATE) : id;
+  if (base < 0 || base >= num_models()) return nullptr;
+  const ModelEntry* e = &registry().models[size_t(base)];
+  if (runtime_id(id) && base < kNumSingle) return nullptr;    // the flag applies to fused aggregates only
+  return e;
+}
+static_assert(kAggregateModeSlot == kMaxParams - 1, "the aggregate mode travels in the parameter block's last slot");
 
 int prepare(int model_id, const float* params, int nparams, size_t n, EvalArgs& a, const ModelEntry*& e)
 {
@@ -407,6 +417,7 @@ int prepare(int model_id, const float* params, int nparams, size_t n, EvalArgs& 
   if (nparams > 0 && !params) return fail(BBM_HIP_ERR_INVALID_ARG, "params is NULL");
   std::memset(&a, 0, sizeof(a));
   for (int i = 0; i < nparams; ++i) a.p.v[i] = params[i];
+  a.p.v[kAggregateModeSlot] = runtime_id(model_id) ? 1.0f : 0.0f;
   a.n = n;
   return BBM_HIP_OK;
 }
@@ -753,6 +764,7 @@ static int prepare_f64(int model_id, const double* params, int nparams, const Mo
   if (nparams > 0 && !params) return fail(BBM_HIP_ERR_INVALID_ARG, "params is NULL");
   std::memset(&p, 0, sizeof(p));
   for (int i = 0; i < nparams; ++i) p.v[i] = params[i];
+  p.v[f64::kMaxParamsF64 - 1] = runtime_id(model_id) ? 1.0 : 0.0;
   return BBM_HIP_OK;
 }
 
@@ -1010,6 +1022,7 @@ int bbm_hip_check(int model_id, const float* params, int nparams, const bbm_hip_
   a.partial = static_cast<double*>(workspace);
   a.counts = reinterpret_cast<unsigned long long*>(counts);
   for (int i = 0; i < nparams; ++i) a.p.v[i] = params[i];
+  a.p.v[kAggregateModeSlot] = runtime_id(model_id) ? 1.0f : 0.0f;
   const hipStream_t s = static_cast<hipStream_t>(stream);
   if (d->test == kCheckSampleCount)
   {

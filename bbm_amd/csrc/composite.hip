@@ -19,6 +19,10 @@
 // registry kernel, its own host-side preparation such as the He family's CDF); the small kernels below only combine
 // per-lane results in the reference's order and rounding (float or double: Value of the configuration).  Scratch
 // is stream-ordered (scratch_acquire / scratch_release): no host synchronisation.
+//
+// A BBM_HIP_AGGREGATE_BSDF node is the reference's runtime aggregatebsdf (include/bbm/aggregatebsdf.h:40-190, what
+// fromString<bsdf_ptr> builds): eval / reflectance as left folds from 0 ((0 + e0) + e1) + ..., pdf as the sum of
+// w_k pdf_k / sum term by term (masked sum > eps), sample masked by sum > eps before the same child selection.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -59,6 +63,33 @@ __global__ __launch_bounds__(kB) void k_fold3(const T* tr, const T* tg, const T*
   BBM_GRID_LOOP(i, n) { r[i] = tr[i] + r[i]; g[i] = tg[i] + g[i]; b[i] = tb[i] + b[i]; }
 }
 
+// aggregatebsdf's left fold (aggregatebsdf.h:79-83, :209-212): acc = (first ? 0 + acc : acc) + t, forward
+template<class T>
+__global__ __launch_bounds__(kB) void k_lfold3(const T* tr, const T* tg, const T* tb, T* r, T* g, T* b, uint64_t n,
+                                               int first)
+{
+  BBM_GRID_LOOP(i, n)
+  {
+    // the accumulation starts from Spectrum(0): 0 + e0 first (-0 becomes +0), then + e_k
+    r[i] = (first ? T(0) + r[i] : r[i]) + tr[i];
+    g[i] = (first ? T(0) + g[i] : g[i]) + tg[i];
+    b[i] = (first ? T(0) + b[i] : b[i]) + tb[i];
+  }
+}
+
+// aggregatebsdf::pdf (aggregatebsdf.h:173-187): pdf = 0; pdf += w_k pdf_k / sum, the lanes with sum <= eps masked
+template<class T>
+__global__ __launch_bounds__(kB) void k_inner_bsdf(const T* p, const T* w, const T* sum, T* ip, uint64_t n, int first)
+{
+  BBM_GRID_LOOP(i, n) ip[i] = (first ? T(0) : ip[i]) + (w[i] * p[i]) / sum[i];
+}
+
+template<class T>
+__global__ __launch_bounds__(kB) void k_mask_sum(const T* ip, const T* sum, T* pdf, uint64_t n)
+{
+  BBM_GRID_LOOP(i, n) pdf[i] = (sum[i] > eps_of<T>()) ? ip[i] : T(0);
+}
+
 // w_k = hsum(reflectance_k) and sum = sum + w_k (forward, from 0)
 template<class T>
 __global__ __launch_bounds__(kB) void k_weight(const T* r, const T* g, const T* b, T* w, T* sum, uint64_t n, int first)
@@ -89,11 +120,12 @@ __global__ __launch_bounds__(kB) void k_mix(const T* ip, const T* sum, T* pdf, u
 // xs = its rescaled xi0
 template<class T>
 __global__ __launch_bounds__(kB) void k_select(const T* w, int nchild, const T* sum, const T* xi0, const uint8_t* mask,
-                                               int8_t* chosen, T* xs, uint64_t n)
+                                               int8_t* chosen, T* xs, uint64_t n, int bsdf)
 {
   BBM_GRID_LOOP(i, n)
   {
-    const bool m0 = mask ? (mask[i] != 0) : true;
+    // aggregatebsdf: mask &= (sum > eps) before the selection (aggregatebsdf.h:115)
+    const bool m0 = (mask ? (mask[i] != 0) : true) && (!bsdf || sum[i] > eps_of<T>());
     T x = xi0[i] * sum[i];
     int c = -1;
     T nx = T(0);
@@ -230,6 +262,20 @@ struct Composite
   using L = Leaf<T>;
   using Child = typename L::Child;
 
+  static bool is_agg(int id) { return id == BBM_HIP_AGGREGATE || id == BBM_HIP_AGGREGATE_BSDF; }
+
+  // the top level: `children` of an aggregatemodel, or (nchild = 1) the root node itself
+  static void root(const Child*& c, int& nchild, bool& bsdf)
+  {
+    bsdf = false;
+    if (c && nchild == 1 && is_agg(c[0].model_id))
+    {
+      bsdf = c[0].model_id == BBM_HIP_AGGREGATE_BSDF;
+      nchild = c[0].nchildren;
+      c = c[0].children;
+    }
+  }
+
   static int check(const Child* c, int nchild, int depth = 0)
   {
     if (depth > kMaxDepth) return fail(BBM_HIP_ERR_INVALID_ARG, "aggregates nested deeper than 16 levels");
@@ -237,7 +283,7 @@ struct Composite
     if (nchild > 127) return fail(BBM_HIP_ERR_INVALID_ARG, "at most 127 children");
     for (int k = 0; k < nchild; ++k)
     {
-      if (c[k].model_id == BBM_HIP_AGGREGATE)
+      if (is_agg(c[k].model_id))
       {
         const int rc = check(c[k].children, c[k].nchildren, depth + 1);
         if (rc) return rc;
@@ -253,34 +299,38 @@ struct Composite
     return BBM_HIP_OK;
   }
 
-  // --- one child, leaf or nested aggregate
+  // --- one child, leaf or nested aggregate (of either kind)
   static int child_eval(const Child& c, const T* ix, const T* iy, const T* iz, const T* ox, const T* oy, const T* oz,
                         const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* r, T* g, T* b, hipStream_t s)
   {
-    if (c.model_id == BBM_HIP_AGGREGATE)
-      return eval_pdf(c.children, c.nchildren, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, r, g, b, nullptr, s);
+    if (is_agg(c.model_id))
+      return eval_pdf(c.children, c.nchildren, c.model_id == BBM_HIP_AGGREGATE_BSDF, ix, iy, iz, ox, oy, oz, mask, n,
+                      comp, unit, r, g, b, nullptr, s);
     return L::eval(c, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, r, g, b, s);
   }
   static int child_pdf(const Child& c, const T* ix, const T* iy, const T* iz, const T* ox, const T* oy, const T* oz,
                        const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* p, hipStream_t s)
   {
-    if (c.model_id == BBM_HIP_AGGREGATE)
-      return eval_pdf(c.children, c.nchildren, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, nullptr, nullptr, nullptr,
-                      p, s);
+    if (is_agg(c.model_id))
+      return eval_pdf(c.children, c.nchildren, c.model_id == BBM_HIP_AGGREGATE_BSDF, ix, iy, iz, ox, oy, oz, mask, n,
+                      comp, unit, nullptr, nullptr, nullptr, p, s);
     return L::pdf(c, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, p, s);
   }
   static int child_reflectance(const Child& c, const T* ox, const T* oy, const T* oz, const uint8_t* mask, size_t n,
                                uint32_t comp, uint32_t unit, T* r, T* g, T* b, hipStream_t s)
   {
-    if (c.model_id == BBM_HIP_AGGREGATE) return reflectance(c.children, c.nchildren, ox, oy, oz, mask, n, comp, unit, r, g, b, s);
+    if (is_agg(c.model_id))
+      return reflectance(c.children, c.nchildren, c.model_id == BBM_HIP_AGGREGATE_BSDF, ox, oy, oz, mask, n, comp, unit,
+                         r, g, b, s);
     return L::reflectance(c, ox, oy, oz, mask, n, comp, unit, r, g, b, s);
   }
   static int child_sample(const Child& c, const T* ox, const T* oy, const T* oz, const T* xi0, const T* xi1,
                           const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* dx, T* dy, T* dz, T* p,
                           uint32_t* f, hipStream_t s)
   {
-    if (c.model_id == BBM_HIP_AGGREGATE)
-      return sample(c.children, c.nchildren, ox, oy, oz, xi0, xi1, mask, n, comp, unit, dx, dy, dz, p, f, s);
+    if (is_agg(c.model_id))
+      return sample(c.children, c.nchildren, c.model_id == BBM_HIP_AGGREGATE_BSDF, ox, oy, oz, xi0, xi1, mask, n, comp,
+                    unit, dx, dy, dz, p, f, s);
     return L::sample(c, ox, oy, oz, xi0, xi1, mask, n, comp, unit, dx, dy, dz, p, f, s);
   }
 
@@ -299,25 +349,50 @@ struct Composite
     return BBM_HIP_OK;
   }
 
-  // pdf = mixture of the children's pdfs at (in, out) with weights w / sum
-  static int mixture_pdf(const Child* c, int nchild, const T* ix, const T* iy, const T* iz, const T* ox, const T* oy,
-                         const T* oz, const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, const T* w,
-                         const T* sum, T* tp, T* ip, T* pdf, hipStream_t s)
+  // pdf = mixture of the children's pdfs at (in, out) with weights w / sum: aggregatemodel's inner product over the
+  // sum, or (bsdf) aggregatebsdf's per-term quotients
+  static int mixture_pdf(const Child* c, int nchild, bool bsdf, const T* ix, const T* iy, const T* iz, const T* ox,
+                         const T* oy, const T* oz, const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit,
+                         const T* w, const T* sum, T* tp, T* ip, T* pdf, hipStream_t s)
   {
     for (int k = 0; k < nchild; ++k)
     {
       int rc = child_pdf(c[k], ix, iy, iz, ox, oy, oz, mask, n, comp, unit, tp, s);
       if (rc) return rc;
-      hipLaunchKernelGGL(k_inner<T>, dim3(grid(n)), dim3(kB), 0, s, tp, w + size_t(k) * n, ip, uint64_t(n), int(k == 0));
+      if (bsdf)
+        hipLaunchKernelGGL(k_inner_bsdf<T>, dim3(grid(n)), dim3(kB), 0, s, tp, w + size_t(k) * n, sum, ip, uint64_t(n),
+                           int(k == 0));
+      else
+        hipLaunchKernelGGL(k_inner<T>, dim3(grid(n)), dim3(kB), 0, s, tp, w + size_t(k) * n, ip, uint64_t(n), int(k == 0));
       if ((rc = launched())) return rc;
     }
-    hipLaunchKernelGGL(k_mix<T>, dim3(grid(n)), dim3(kB), 0, s, ip, sum, pdf, uint64_t(n));
+    if (bsdf) hipLaunchKernelGGL(k_mask_sum<T>, dim3(grid(n)), dim3(kB), 0, s, ip, sum, pdf, uint64_t(n));
+    else hipLaunchKernelGGL(k_mix<T>, dim3(grid(n)), dim3(kB), 0, s, ip, sum, pdf, uint64_t(n));
     return launched();
   }
 
-  static int eval_pdf(const Child* c, int nchild, const T* ix, const T* iy, const T* iz, const T* ox, const T* oy,
-                      const T* oz, const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* r, T* g, T* b,
-                      T* pdf, hipStream_t s)
+  // the children's sum: aggregatemodel's right fold e0 + (e1 + (... + eK)), or (bsdf) aggregatebsdf's left fold
+  // ((0 + e0) + e1) + ... ; `part` evaluates child k into the given outputs
+  template<class F>
+  static int fold(int nchild, bool bsdf, size_t n, T* r, T* g, T* b, T* tr, T* tg, T* tb, hipStream_t s, F&& part)
+  {
+    int rc;
+    const int last = nchild - 1;
+    if ((rc = part(bsdf ? 0 : last, r, g, b))) return rc;
+    for (int j = 1; j <= last; ++j)
+    {
+      const int k = bsdf ? j : last - j;
+      if ((rc = part(k, tr, tg, tb))) return rc;
+      if (bsdf) hipLaunchKernelGGL(k_lfold3<T>, dim3(grid(n)), dim3(kB), 0, s, tr, tg, tb, r, g, b, uint64_t(n), int(j == 1));
+      else hipLaunchKernelGGL(k_fold3<T>, dim3(grid(n)), dim3(kB), 0, s, tr, tg, tb, r, g, b, uint64_t(n));
+      if ((rc = launched())) return rc;
+    }
+    return BBM_HIP_OK;
+  }
+
+  static int eval_pdf(const Child* c, int nchild, bool bsdf, const T* ix, const T* iy, const T* iz, const T* ox,
+                      const T* oy, const T* oz, const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* r, T* g,
+                      T* b, T* pdf, hipStream_t s)
   {
     Scratch sc(s);
     T* tr = sc.get<T>(n);
@@ -325,18 +400,10 @@ struct Composite
     T* tb = sc.get<T>(n);
     if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
     int rc;
-    if (r)
-    {
-      // right fold: the last child straight into the output, then e_k + acc for k = K-2 .. 0
-      const int last = nchild - 1;
-      if ((rc = child_eval(c[last], ix, iy, iz, ox, oy, oz, mask, n, comp, unit, r, g, b, s))) return rc;
-      for (int k = last - 1; k >= 0; --k)
-      {
-        if ((rc = child_eval(c[k], ix, iy, iz, ox, oy, oz, mask, n, comp, unit, tr, tg, tb, s))) return rc;
-        hipLaunchKernelGGL(k_fold3<T>, dim3(grid(n)), dim3(kB), 0, s, tr, tg, tb, r, g, b, uint64_t(n));
-        if ((rc = launched())) return rc;
-      }
-    }
+    if (r && (rc = fold(nchild, bsdf, n, r, g, b, tr, tg, tb, s, [&](int k, T* rr, T* gg, T* bb) {
+          return child_eval(c[k], ix, iy, iz, ox, oy, oz, mask, n, comp, unit, rr, gg, bb, s);
+        })))
+      return rc;
     if (pdf)
     {
       T* w = sc.get<T>(size_t(nchild) * n);
@@ -344,34 +411,28 @@ struct Composite
       T* ip = sc.get<T>(n);
       if (!w || !sum || !ip) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
       if ((rc = weights(c, nchild, ox, oy, oz, mask, n, comp, unit, w, sum, tr, tg, tb, s))) return rc;
-      if ((rc = mixture_pdf(c, nchild, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, w, sum, tr, ip, pdf, s))) return rc;
+      if ((rc = mixture_pdf(c, nchild, bsdf, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, w, sum, tr, ip, pdf, s)))
+        return rc;
     }
     return BBM_HIP_OK;
   }
 
-  static int reflectance(const Child* c, int nchild, const T* ox, const T* oy, const T* oz, const uint8_t* mask,
-                         size_t n, uint32_t comp, uint32_t unit, T* r, T* g, T* b, hipStream_t s)
+  static int reflectance(const Child* c, int nchild, bool bsdf, const T* ox, const T* oy, const T* oz,
+                         const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* r, T* g, T* b, hipStream_t s)
   {
     Scratch sc(s);
     T* tr = sc.get<T>(n);
     T* tg = sc.get<T>(n);
     T* tb = sc.get<T>(n);
     if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
-    const int last = nchild - 1;
-    int rc;
-    if ((rc = child_reflectance(c[last], ox, oy, oz, mask, n, comp, unit, r, g, b, s))) return rc;
-    for (int k = last - 1; k >= 0; --k)
-    {
-      if ((rc = child_reflectance(c[k], ox, oy, oz, mask, n, comp, unit, tr, tg, tb, s))) return rc;
-      hipLaunchKernelGGL(k_fold3<T>, dim3(grid(n)), dim3(kB), 0, s, tr, tg, tb, r, g, b, uint64_t(n));
-      if ((rc = launched())) return rc;
-    }
-    return BBM_HIP_OK;
+    return fold(nchild, bsdf, n, r, g, b, tr, tg, tb, s, [&](int k, T* rr, T* gg, T* bb) {
+      return child_reflectance(c[k], ox, oy, oz, mask, n, comp, unit, rr, gg, bb, s);
+    });
   }
 
-  static int sample(const Child* c, int nchild, const T* ox, const T* oy, const T* oz, const T* xi0, const T* xi1,
-                    const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* dx, T* dy, T* dz, T* pdf,
-                    uint32_t* flag, hipStream_t s)
+  static int sample(const Child* c, int nchild, bool bsdf, const T* ox, const T* oy, const T* oz, const T* xi0,
+                    const T* xi1, const uint8_t* mask, size_t n, uint32_t comp, uint32_t unit, T* dx, T* dy, T* dz,
+                    T* pdf, uint32_t* flag, hipStream_t s)
   {
     Scratch sc(s);
     T* w = sc.get<T>(size_t(nchild) * n);
@@ -389,7 +450,8 @@ struct Composite
       return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
     int rc;
     if ((rc = weights(c, nchild, ox, oy, oz, mask, n, comp, unit, w, sum, t0, t1, t2, s))) return rc;
-    hipLaunchKernelGGL(k_select<T>, dim3(grid(n)), dim3(kB), 0, s, w, nchild, sum, xi0, mask, chosen, xs, uint64_t(n));
+    hipLaunchKernelGGL(k_select<T>, dim3(grid(n)), dim3(kB), 0, s, w, nchild, sum, xi0, mask, chosen, xs, uint64_t(n),
+                       int(bsdf));
     hipLaunchKernelGGL(k_zero_sample<T>, dim3(grid(n)), dim3(kB), 0, s, dx, dy, dz, flag, uint64_t(n));
     if ((rc = launched())) return rc;
     for (int k = 0; k < nchild; ++k)
@@ -401,8 +463,9 @@ struct Composite
                          uint64_t(n));
       if ((rc = launched())) return rc;
     }
-    // pdf of the sampled direction: the weighted mixture of every child's pdf (:116-117)
-    return mixture_pdf(c, nchild, dx, dy, dz, ox, oy, oz, mask, n, comp, unit, w, sum, t3, ip, pdf, s);
+    // pdf of the sampled direction: the weighted mixture of every child's pdf (:116-117; aggregatebsdf.h:133-137,
+    // where a lane without a sample keeps pdf 0: sum <= eps there, which the mixture masks)
+    return mixture_pdf(c, nchild, bsdf, dx, dy, dz, ox, oy, oz, mask, n, comp, unit, w, sum, t3, ip, pdf, s);
   }
 };
 
@@ -418,12 +481,14 @@ int bbm_hip_aggregate_eval_pdf(const bbm_hip_child* children, int nchildren, con
                                const uint8_t* mask, size_t n, uint32_t component, uint32_t unit, float* r, float* g,
                                float* b, float* pdf, void* stream)
 {
+  bool bsdf;
+  Composite<float>::root(children, nchildren, bsdf);
   int rc = Composite<float>::check(children, nchildren);
   if (rc) return rc;
   if (!r && !pdf) return fail(BBM_HIP_ERR_INVALID_ARG, "no output requested (rgb and pdf are NULL)");
   if (r && (!g || !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "eval output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<float>::eval_pdf(children, nchildren, in_x, in_y, in_z, out_x, out_y, out_z, mask, n, component,
+  return Composite<float>::eval_pdf(children, nchildren, bsdf, in_x, in_y, in_z, out_x, out_y, out_z, mask, n, component,
                                     unit, r, g, b, pdf, static_cast<hipStream_t>(stream));
 }
 
@@ -431,11 +496,13 @@ int bbm_hip_aggregate_reflectance(const bbm_hip_child* children, int nchildren, 
                                   const float* out_y, const float* out_z, const uint8_t* mask, size_t n,
                                   uint32_t component, uint32_t unit, float* r, float* g, float* b, void* stream)
 {
+  bool bsdf;
+  Composite<float>::root(children, nchildren, bsdf);
   int rc = Composite<float>::check(children, nchildren);
   if (rc) return rc;
   if (!r || !g || !b) return fail(BBM_HIP_ERR_INVALID_ARG, "output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<float>::reflectance(children, nchildren, out_x, out_y, out_z, mask, n, component, unit, r, g, b,
+  return Composite<float>::reflectance(children, nchildren, bsdf, out_x, out_y, out_z, mask, n, component, unit, r, g, b,
                                        static_cast<hipStream_t>(stream));
 }
 
@@ -444,12 +511,14 @@ int bbm_hip_aggregate_sample(const bbm_hip_child* children, int nchildren, const
                              uint32_t component, uint32_t unit, float* dir_x, float* dir_y, float* dir_z, float* pdf,
                              uint32_t* flag, void* stream)
 {
+  bool bsdf;
+  Composite<float>::root(children, nchildren, bsdf);
   int rc = Composite<float>::check(children, nchildren);
   if (rc) return rc;
   if (!xi0 || !xi1 || !dir_x || !dir_y || !dir_z || !pdf || !flag)
     return fail(BBM_HIP_ERR_INVALID_ARG, "xi / output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<float>::sample(children, nchildren, out_x, out_y, out_z, xi0, xi1, mask, n, component, unit, dir_x,
+  return Composite<float>::sample(children, nchildren, bsdf, out_x, out_y, out_z, xi0, xi1, mask, n, component, unit, dir_x,
                                   dir_y, dir_z, pdf, flag, static_cast<hipStream_t>(stream));
 }
 
@@ -458,12 +527,14 @@ int bbm_hip_aggregate_eval_pdf_f64(const bbm_hip_child_f64* children, int nchild
                                    const double* out_z, const uint8_t* mask, size_t n, uint32_t component,
                                    uint32_t unit, double* r, double* g, double* b, double* pdf, void* stream)
 {
+  bool bsdf;
+  Composite<double>::root(children, nchildren, bsdf);
   int rc = Composite<double>::check(children, nchildren);
   if (rc) return rc;
   if (!r && !pdf) return fail(BBM_HIP_ERR_INVALID_ARG, "no output requested (rgb and pdf are NULL)");
   if (r && (!g || !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "eval output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<double>::eval_pdf(children, nchildren, in_x, in_y, in_z, out_x, out_y, out_z, mask, n, component,
+  return Composite<double>::eval_pdf(children, nchildren, bsdf, in_x, in_y, in_z, out_x, out_y, out_z, mask, n, component,
                                      unit, r, g, b, pdf, static_cast<hipStream_t>(stream));
 }
 
@@ -471,11 +542,13 @@ int bbm_hip_aggregate_reflectance_f64(const bbm_hip_child_f64* children, int nch
                                       const double* out_y, const double* out_z, const uint8_t* mask, size_t n,
                                       uint32_t component, uint32_t unit, double* r, double* g, double* b, void* stream)
 {
+  bool bsdf;
+  Composite<double>::root(children, nchildren, bsdf);
   int rc = Composite<double>::check(children, nchildren);
   if (rc) return rc;
   if (!r || !g || !b) return fail(BBM_HIP_ERR_INVALID_ARG, "output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<double>::reflectance(children, nchildren, out_x, out_y, out_z, mask, n, component, unit, r, g, b,
+  return Composite<double>::reflectance(children, nchildren, bsdf, out_x, out_y, out_z, mask, n, component, unit, r, g, b,
                                         static_cast<hipStream_t>(stream));
 }
 
@@ -484,12 +557,14 @@ int bbm_hip_aggregate_sample_f64(const bbm_hip_child_f64* children, int nchildre
                                  const uint8_t* mask, size_t n, uint32_t component, uint32_t unit, double* dir_x,
                                  double* dir_y, double* dir_z, double* pdf, uint32_t* flag, void* stream)
 {
+  bool bsdf;
+  Composite<double>::root(children, nchildren, bsdf);
   int rc = Composite<double>::check(children, nchildren);
   if (rc) return rc;
   if (!xi0 || !xi1 || !dir_x || !dir_y || !dir_z || !pdf || !flag)
     return fail(BBM_HIP_ERR_INVALID_ARG, "xi / output pointer is NULL");
   if (n == 0) return BBM_HIP_OK;
-  return Composite<double>::sample(children, nchildren, out_x, out_y, out_z, xi0, xi1, mask, n, component, unit, dir_x,
+  return Composite<double>::sample(children, nchildren, bsdf, out_x, out_y, out_z, xi0, xi1, mask, n, component, unit, dir_x,
                                    dir_y, dir_z, pdf, flag, static_cast<hipStream_t>(stream));
 }
 

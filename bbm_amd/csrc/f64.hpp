@@ -36,6 +36,8 @@
 namespace bbmhip {
 namespace f64 {
 
+constexpr int kMaxParamsF64 = 64;      // parameter block size; the last slot carries the aggregate mode (Aggregate)
+
 constexpr double kEps = 2.220446049250313080847263336181640625e-16;   // numeric_limits<double>::epsilon()
 constexpr double kPi = 3.141592653589793115997963468544185161590576171875;          // std::numbers::pi (double)
 constexpr double kInvPi = 0.31830988618379069121644420192751567810773849487304688;  // std::numbers::inv_pi
@@ -745,7 +747,8 @@ struct Aggregate
   static constexpr int kF64Waves = heavy_f64<A>() > heavy_f64<B>() ? heavy_f64<A>() : heavy_f64<B>();
   A a;
   B b;
-  __device__ explicit Aggregate(const double* p) : a(p), b(p + A::kParams) {}
+  bool runtime;            // aggregatebsdf semantics (bbm_amd/csrc/aggregate.hpp): the parameter block's last slot
+  __device__ explicit Aggregate(const double* p) : a(p), b(p + A::kParams), runtime(p[kMaxParamsF64 - 1] != 0.0) {}
   __device__ __forceinline__ void eval_pdf(d3 in, d3 out, uint32_t component, double* rgb, double& pdf) const
   {
     double ra[3], rb[3], pa, pb;
@@ -766,12 +769,13 @@ struct Aggregate
     wa = ((0.0 + ra[0]) + ra[1]) + ra[2];
     wb = ((0.0 + rb[0]) + rb[1]) + rb[2];
   }
-  // inner_product(pdfs, weights, 0) / sum, masked sum > eps (:141-142)
-  __device__ __forceinline__ static double mix(double pa, double pb, double wa, double wb)
+  // inner_product(pdfs, weights, 0) / sum, masked sum > eps (:141-142); aggregatebsdf: w_k pdf_k / sum per term
+  __device__ __forceinline__ double mix(double pa, double pb, double wa, double wb) const
   {
     const double sum = (0.0 + wa) + wb;
-    const double ip = (0.0 + pa * wa) + pb * wb;
-    return (sum > kEps) ? ip / sum : 0.0;
+    if (!(sum > kEps)) return 0.0;
+    if (runtime) return (0.0 + wa * pa / sum) + wb * pb / sum;
+    return ((0.0 + pa * wa) + pb * wb) / sum;
   }
   // :81-113: the child claiming xi0 * sum (a later child that also claims it wins), pdf of the mixture
   __device__ __forceinline__ void sample(d3 out, double xi0, double xi1, uint32_t component, d3& dir, double& pdf,
@@ -783,6 +787,7 @@ struct Aggregate
     if (!component) return;
     double wa, wb, p;
     weights(out, component, wa, wb);
+    if (runtime && !((0.0 + wa) + wb > kEps)) return;      // aggregatebsdf's bail-out (aggregatebsdf.h:115-116)
     double x = xi0 * ((0.0 + wa) + wb);
     if ((x >= 0) && (x <= wa)) a.sample(out, (wa > kEps) ? x / wa : 0.0, xi1, component, dir, p, flag);
     x -= wa;
@@ -1747,7 +1752,6 @@ using AggNganHeM = Aggregate<Lambertian, NganHeM>;
 
 // ------------------------------------------------------------------------------------------------- kernels
 
-constexpr int kMaxParamsF64 = 64;
 struct ParamBlockF64 { double v[kMaxParamsF64]; };
 
 struct EvalArgsF64

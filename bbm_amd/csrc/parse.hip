@@ -235,6 +235,14 @@ bool parse_any(Parser& p, Node& node, int& code)
   return true;
 }
 
+// registry id of a parsed leaf: every "Aggregate(...)" of a string is the runtime aggregatebsdf
+// (bsdf_string_convert.h:59), so a fused aggregate's id carries BBM_HIP_RUNTIME_AGGREGATE
+int string_id(const std::string& name)
+{
+  const int id = bbm_hip_model_id(name.c_str());
+  return (id >= 0 && name.rfind("Aggregate<", 0) == 0) ? (id | BBM_HIP_RUNTIME_AGGREGATE) : id;
+}
+
 // preorder flattening for bbm_hip_parse_model_tree
 void preorder(const Node& n, std::vector<const Node*>& out)
 {
@@ -290,7 +298,7 @@ int bbm_hip_parse_model(const char* str, int* model_ids, float* params, int* npa
   int off = 0;
   for (size_t c = 0; c < kids.size(); ++c)
   {
-    if (model_ids) model_ids[c] = bbm_hip_model_id(kids[c]->name.c_str());
+    if (model_ids) model_ids[c] = string_id(kids[c]->name);
     if (nparams) nparams[c] = int(kids[c]->params.size());
     for (float v : kids[c]->params) if (params) params[off++] = v;
   }
@@ -316,7 +324,7 @@ int bbm_hip_parse_model_tree(const char* str, int* model_ids, int* nchildren, fl
   for (size_t k = 0; k < nodes.size(); ++k)
   {
     const Node& n = *nodes[k];
-    if (model_ids) model_ids[k] = n.composed() ? BBM_HIP_AGGREGATE : bbm_hip_model_id(n.leaf.name.c_str());
+    if (model_ids) model_ids[k] = n.composed() ? BBM_HIP_AGGREGATE_BSDF : string_id(n.leaf.name);
     if (nchildren) nchildren[k] = int(n.kids.size());
     if (nparams) nparams[k] = int(n.leaf.params.size());
     for (float v : n.leaf.params) if (params) params[off++] = v;

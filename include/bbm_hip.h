@@ -161,13 +161,24 @@ int bbm_hip_reflectance_f64(int model_id, const double* params, int nparams,
  * member functions would).  Same conventions as the single-model entry points; `r` may be NULL in
  * bbm_hip_aggregate_eval_pdf for pdf only, `pdf` NULL for eval only. */
 #define BBM_HIP_AGGREGATE (-100)
+/* The reference's RUNTIME aggregate, aggregatebsdf (include/bbm/aggregatebsdf.h:40-190): what fromString<bsdf_ptr> /
+ * bsdf_import builds from "Aggregate(...)" (bsdf_string_convert.h:59), i.e. what checkBsdf, plotBsdf and the
+ * Mitsuba plugin evaluate.  It differs from aggregatemodel in rounding and in one behaviour: eval and reflectance
+ * are LEFT folds from 0, the pdf adds w_k pdf_k / sum term by term, and sample returns no sample (here {0, 0, None};
+ * the reference's is indeterminate) unless sum > eps.  As a node kind in a child tree; as a flag OR-ed into the model
+ * id of a fused Aggregate<A,B> entry (bbm_hip_eval / _pdf / _eval_pdf / _sample / _reflectance / _check and their
+ * _f64 forms), the fused kernel takes these semantics.  bbm_hip_parse_model(_tree) returns both for strings. */
+#define BBM_HIP_AGGREGATE_BSDF (-101)
+#define BBM_HIP_RUNTIME_AGGREGATE 0x40000000
+/* A tree may also be passed as its root alone: nchildren = 1 and children[0] an aggregate node (BBM_HIP_AGGREGATE
+ * or BBM_HIP_AGGREGATE_BSDF) -- the only way to give the top level aggregatebsdf semantics. */
 typedef struct bbm_hip_child
 {
-  int model_id;                            /* registry id, or BBM_HIP_AGGREGATE */
+  int model_id;                            /* registry id (may carry BBM_HIP_RUNTIME_AGGREGATE), or an aggregate node */
   const float* params;                     /* host memory, nparams floats (bbm_hip_model_nparams); aggregate: NULL */
   int nparams;                             /* aggregate: 0 */
-  const struct bbm_hip_child* children;    /* BBM_HIP_AGGREGATE: its children; else NULL */
-  int nchildren;                           /* BBM_HIP_AGGREGATE: >= 2; else 0 */
+  const struct bbm_hip_child* children;    /* aggregate node: its children; else NULL */
+  int nchildren;                           /* aggregate node: >= 2; else 0 */
 } bbm_hip_child;
 
 int bbm_hip_aggregate_eval_pdf(const bbm_hip_child* children, int nchildren,
@@ -221,18 +232,21 @@ const char* bbm_hip_model_layout(int model_id);
 /* Parse a model string -- bbm::toString form, an entry of the fits/ files, `Aggregate(child, child, ...)` -- as the
  * reference's runtime fromString does (include/bbm/bsdf_string_convert.h:52-85; the handle behind bsdf_ptr,
  * checkBsdf and the Mitsuba plugin).  A single model or an aggregate with a fused kernel yields ONE entry
- * (model_ids[0], its nparams[0] parameters); any other aggregate yields one entry per child, to be evaluated
- * with bbm_hip_aggregate_* (a child may be a fused aggregate).  Parameters are written back to back into params.
+ * (model_ids[0], its nparams[0] parameters; a fused aggregate's id carries BBM_HIP_RUNTIME_AGGREGATE); any other
+ * aggregate yields one entry per child, to be evaluated with bbm_hip_aggregate_* as the children of a
+ * BBM_HIP_AGGREGATE_BSDF root node (a child may be a fused aggregate).  Parameters are written back to back into params.
  * Returns the number of entries (>= 1) or an error code (unknown model / attribute, malformed string, value beyond
  * the float range; BBM_HIP_ERR_UNSUPPORTED for a composed aggregate nested inside another: use
  * bbm_hip_parse_model_tree). */
 int bbm_hip_parse_model(const char* str, int* model_ids, float* params, int* nparams, int max_children,
                         int params_capacity);
 
-/* The same for any nesting, as a tree in preorder: node k is model_ids[k] (a registry id, or BBM_HIP_AGGREGATE
+/* The same for any nesting, as a tree in preorder: node k is model_ids[k] (a registry id, or BBM_HIP_AGGREGATE_BSDF
  * for a composed aggregate, whose nchildren[k] >= 2 children follow it in preorder; 0 for a registry model) with
- * nparams[k] parameters (0 for BBM_HIP_AGGREGATE) written back to back into params.  A string without a composed
- * aggregate gives one node.  Returns the node count or an error code. */
+ * nparams[k] parameters (0 for an aggregate node) written back to back into params.  A string without a composed
+ * aggregate gives one node.  Every "Aggregate(...)" of a string is the runtime aggregatebsdf, as in the reference:
+ * composed ones are BBM_HIP_AGGREGATE_BSDF nodes, fused ones carry BBM_HIP_RUNTIME_AGGREGATE in their id (in
+ * bbm_hip_parse_model too).  Returns the node count or an error code. */
 int bbm_hip_parse_model_tree(const char* str, int* model_ids, int* nchildren, float* params, int* nparams,
                              int max_nodes, int params_capacity);
 

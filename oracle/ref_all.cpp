@@ -5,3 +5,4 @@
 #include "ref_fit.cpp"
 #include "ref_check.cpp"
 #include "ref_merl.cpp"
+#include "ref_runtime.cpp"

@@ -41,6 +41,8 @@
 #include "ndf/epd.h"
 #include "maskingshadowing/vanginneken.h"
 #include "ref_he.hpp"
+#include "bbm/bsdf_ptr.h"
+#include "bbm/aggregatebsdf.h"
 
 #include <cstdint>
 #include <cstring>
@@ -221,6 +223,13 @@ struct ops
     }
   }
 
+  // bbm::make_bsdf_ptr of the model at these parameters (bsdf_ptr.h:218-224): a leaf of the runtime aggregate
+  // fromString<bsdf_ptr> builds (bsdf_string_convert.h:52-82); `out` is a bbm::bsdf_ptr<Config>*
+  static void make_ptr(const float* p, int np, void* out)
+  {
+    *static_cast<bbm::bsdf_ptr<bbm::get_config<M>>*>(out) = bbm::make_bsdf_ptr(make(p, np));
+  }
+
   template<typename OUT>
   static void reflectance(const float* p, int np, size_t n, const float* ox, const float* oy, const float* oz,
                           uint32_t component, uint32_t unit, OUT* r, OUT* g, OUT* b)
@@ -250,6 +259,9 @@ struct entry
   void (*sample_d)(const float*, int, size_t, const float*, const float*, const float*, const float*, const float*, uint32_t, uint32_t, double*, double*, double*, double*, uint32_t*, int) = nullptr;
   // doubleRGB eval / pdf at double directions (the per-lane proofs of the f64 kernels perturb directions in double)
   void (*evalpdf_dd)(const float*, int, size_t, const double*, const double*, const double*, const double*, const double*, const double*, uint32_t, uint32_t, int, double*, double*, double*, double*, int) = nullptr;
+  // bsdf_ptr<floatRGB> / bsdf_ptr<doubleRGB> of the model (ref_runtime.cpp: runtime aggregates)
+  void (*ptr_f)(const float*, int, void*) = nullptr;
+  void (*ptr_d)(const float*, int, void*) = nullptr;
 };
 
 #define BBMREF_ENTRY(MODEL) BBMREF_ENTRY_NS(bbm, MODEL)
@@ -265,7 +277,9 @@ struct entry
          &ops<NS::MODEL<bbm::floatRGB>>::from_string, \
          &ops<NS::MODEL<bbm::doubleRGB>>::template reflectance<double>, \
          &ops<NS::MODEL<bbm::doubleRGB>>::template sample<double>, \
-         &ops<NS::MODEL<bbm::doubleRGB>>::template evalpdf<double, double> }
+         &ops<NS::MODEL<bbm::doubleRGB>>::template evalpdf<double, double>, \
+         &ops<NS::MODEL<bbm::floatRGB>>::make_ptr, \
+         &ops<NS::MODEL<bbm::doubleRGB>>::make_ptr }
 
 
 } // namespace bbmref

@@ -19,6 +19,7 @@
 #include "bbm/bsdf_enumerate.h"
 #include "bbm/bsdf_ptr.h"
 #include "bbm/bsdf.h"
+#include "bbm/aggregatebsdf.h"
 #include "bsdfmodel/scaledmodel.h"
 #include "bsdfmodel/microfacet.h"
 #include "bsdfmodel/aggregatemodel.h"
@@ -123,6 +124,31 @@ static std::vector<int> ids(const bbm::hip::basic_model_desc<T>& d)
   return v;
 }
 
+// the same with the aggregate semantics erased (runtime aggregatebsdf -> aggregatemodel): what a string and the
+// template type must agree on
+static int plain(int id)
+{
+  if(id == BBM_HIP_AGGREGATE_BSDF) return BBM_HIP_AGGREGATE;
+  return id >= 0 ? (id & ~BBM_HIP_RUNTIME_AGGREGATE) : id;
+}
+template<typename T>
+static std::vector<int> plain_ids(const bbm::hip::basic_model_desc<T>& d)
+{
+  std::vector<int> v = ids(d);
+  for(int& i : v) i = plain(i);
+  return v;
+}
+// every aggregate of a string is the runtime aggregatebsdf (bsdf_string_convert.h:59)
+template<typename T>
+static bool runtime_everywhere(const bbm::hip::basic_model_desc<T>& d)
+{
+  if(d.id == BBM_HIP_AGGREGATE) return false;
+  if(d.id >= 0 && std::string(bbm_hip_model_name(d.id)).rfind("Aggregate<", 0) == 0 && !(d.id & BBM_HIP_RUNTIME_AGGREGATE))
+    return false;
+  for(const auto& k : d.kids) if(!runtime_everywhere(k)) return false;
+  return true;
+}
+
 // parameters of the leaves in preorder
 template<typename T>
 static std::vector<T> cat(const bbm::hip::basic_model_desc<T>& d)
@@ -176,12 +202,15 @@ static void check_dispatch(const MODEL& m)
     if(got != flat<float>(m)) { ok = false; why = "describe(model): parameters differ from bbm::parameter_values"; }
     // by string: the same entries, and the values the reference's own fromString reads from that string
     // (toString prints 6 significant digits, so a perturbed model does not round-trip exactly)
-    if(ids(by_string) != ids(by_type)) { ok = false; why = "from_string(toString(model)) picks other kernels"; }
+    if(plain_ids(by_string) != ids(by_type)) { ok = false; why = "from_string(toString(model)) picks other kernels"; }
+    if(!runtime_everywhere(by_string)) { ok = false; why = "from_string: an aggregate without aggregatebsdf semantics"; }
     if(cat(by_string) != flat<float>(bbm::fromString<MODEL>(str))) { ok = false; why = "from_string: parameters differ from bbm::fromString"; }
     if constexpr (WithPtr)
     {
+      // a bsdf_ptr to the template model: the template's (aggregatemodel) semantics at the string's values
       const auto ptr = bbm::make_bsdf_ptr(m);
-      if(!same(bbm::hip::describe(ptr), by_string)) { ok = false; why = "bsdf_ptr resolves differently"; }
+      const auto by_ptr = bbm::hip::describe(ptr);
+      if(ids(by_ptr) != ids(by_type) || cat(by_ptr) != cat(by_string)) { ok = false; why = "bsdf_ptr resolves differently"; }
     }
     std::printf("{\"model\": \"%s\", \"entries\": %zu, \"kernel\": \"%s\", \"nparams\": %zu, \"ok\": %s%s%s%s}\n", str.c_str(),
                 leaves(by_type), bbm_hip_model_name(first_leaf(by_type)), got.size(), ok ? "true" : "false",
@@ -230,6 +259,18 @@ int main()
     const auto d = bbm::hip::describe(bbm::aggregatemodel<bbm::lambertian<F>, bbmref::nganhe<F>>());
     const auto c = bbm::hip::describe(bbm::aggregatemodel<bbm::cooktorrance<F>, bbm::ggx<F>>());
     if(d.composed() || std::string(bbm_hip_model_name(d.id)) != "Aggregate<Lambertian,NganHe>" || !c.composed()) ++failures;
+  }
+  // the runtime aggregate (aggregatebsdf of bsdf_ptrs, what fromString<bsdf_ptr> builds): its bsdf_ptr keeps the
+  // parser's aggregatebsdf semantics -- a flagged fused id for two children, a BBM_HIP_AGGREGATE_BSDF node otherwise
+  {
+    const auto l = bbm::make_bsdf_ptr(bbm::lambertian<F>()), c = bbm::make_bsdf_ptr(bbm::cooktorrance<F>());
+    const auto g = bbm::make_bsdf_ptr(bbm::ggx<F>());
+    const auto two = bbm::hip::describe(bbm::make_bsdf_ptr(bbm::aggregatebsdf<F>(l, c)));
+    const auto three = bbm::hip::describe(bbm::make_bsdf_ptr(bbm::aggregatebsdf<F>(l, c, g)));
+    const bool ok = !two.composed() && (two.id & BBM_HIP_RUNTIME_AGGREGATE) && three.id == BBM_HIP_AGGREGATE_BSDF &&
+                    three.kids.size() == 3 && runtime_everywhere(two) && runtime_everywhere(three);
+    std::printf("{\"runtime_aggregate_ptr\": %s}\n", ok ? "true" : "false");
+    if(!ok) ++failures;
   }
   // nested aggregates (aggregatemodel_base takes any bsdfmodel child, aggregatemodel.h:22): a composed inner
   // aggregate stays one composed child, a fused one stays one registry entry

@@ -685,3 +685,96 @@ def ref_merl_to_string(filename):
     if lib.bbmref_merl_to_string(str(filename).encode(), buf, 4096) < 0:
         raise RuntimeError(f"reference rejected MERL file {filename}")
     return buf.value.decode()
+
+
+# ------------------------------------------------------------------ runtime aggregates (oracle/ref_runtime.cpp)
+
+def runtime_tree(tree):
+    """Preorder arrays of a runtime-aggregate tree: `tree` is (name, params) for a model or ("Aggregate", [kids])."""
+    names, nkids, nps, params = [], [], [], []
+
+    def walk(t):
+        if t[0] == "Aggregate":
+            names.append(b"Aggregate")
+            nkids.append(len(t[1]))
+            nps.append(0)
+            for k in t[1]:
+                walk(k)
+        else:
+            p = np.asarray(t[1], np.float32).reshape(-1)
+            names.append(t[0].encode())
+            nkids.append(0)
+            nps.append(p.size)
+            params.append(p)
+    walk(tree)
+    arr = (ctypes.c_char_p * len(names))(*names)
+    return (len(names), arr, (ctypes.c_int * len(nkids))(*nkids),
+            np.ascontiguousarray(np.concatenate(params) if params else np.zeros(0), np.float32),
+            (ctypes.c_int * len(nps))(*nps))
+
+
+def ref_runtime_eval_pdf(tree, din, dout, component=3, unit=0, nthreads=8, f64=False):
+    """(4, N): eval RGB + pdf of the reference's runtime aggregate (aggregatebsdf of bsdf_ptrs, what
+    fromString<bsdf_ptr> builds), floatRGB (float32 directions) or doubleRGB (f64: float64 directions)."""
+    lib = ref()
+    k, names, nk, params, nps = runtime_tree(tree)
+    dt = np.float64 if f64 else np.float32
+    din = np.ascontiguousarray(din, dtype=dt)
+    dout = np.ascontiguousarray(dout, dtype=dt)
+    n = din.shape[1]
+    res = np.zeros((4, n), dt)
+    fn = lib.bbmref_runtime_eval_pdf_dd if f64 else lib.bbmref_runtime_eval_pdf
+    rc = fn(k, names, nk, _fp(params), nps, ctypes.c_size_t(n), _fp(din[0]), _fp(din[1]), _fp(din[2]), _fp(dout[0]),
+            _fp(dout[1]), _fp(dout[2]), ctypes.c_uint32(component), ctypes.c_uint32(unit), 3, _fp(res[0]), _fp(res[1]),
+            _fp(res[2]), _fp(res[3]), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle cannot build the runtime aggregate {tree!r}")
+    return res
+
+
+def ref_runtime_sample(tree, dout, xi, component=3, unit=0, nthreads=8, f64=False):
+    """((4, N) direction + pdf, (N,) flags) of the reference's runtime aggregate's sample."""
+    lib = ref()
+    k, names, nk, params, nps = runtime_tree(tree)
+    dt = np.float64 if f64 else np.float32
+    dout = np.ascontiguousarray(dout, dtype=dt)
+    xi = np.ascontiguousarray(xi, dtype=dt)
+    n = dout.shape[1]
+    res = np.zeros((4, n), dt)
+    flag = np.zeros(n, np.uint32)
+    fn = lib.bbmref_runtime_sample_dd if f64 else lib.bbmref_runtime_sample
+    rc = fn(k, names, nk, _fp(params), nps, ctypes.c_size_t(n), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]), _fp(xi[0]),
+            _fp(xi[1]), ctypes.c_uint32(component), ctypes.c_uint32(unit), _fp(res[0]), _fp(res[1]), _fp(res[2]),
+            _fp(res[3]), flag.ctypes.data_as(ctypes.c_void_p), nthreads)
+    if rc != 0:
+        raise KeyError(f"oracle cannot build the runtime aggregate {tree!r}")
+    return res, flag
+
+
+def ref_runtime_reflectance(tree, dout, component=3, unit=0, f64=False):
+    lib = ref()
+    k, names, nk, params, nps = runtime_tree(tree)
+    dt = np.float64 if f64 else np.float32
+    dout = np.ascontiguousarray(dout, dtype=dt)
+    n = dout.shape[1]
+    res = np.zeros((3, n), dt)
+    fn = lib.bbmref_runtime_reflectance_dd if f64 else lib.bbmref_runtime_reflectance
+    rc = fn(k, names, nk, _fp(params), nps, ctypes.c_size_t(n), _fp(dout[0]), _fp(dout[1]), _fp(dout[2]),
+            ctypes.c_uint32(component), ctypes.c_uint32(unit), _fp(res[0]), _fp(res[1]), _fp(res[2]))
+    if rc != 0:
+        raise KeyError(f"oracle cannot build the runtime aggregate {tree!r}")
+    return res
+
+
+def runtime_fit_tree(key, params):
+    """The runtime-aggregate tree (runtime_tree) of a fused key "Aggregate<A,B>" at its flat parameter vector: what
+    bsdf_import builds from the material's fits/ line."""
+    names = key[len("Aggregate<"):-1].split(",")
+    p = np.asarray(params, np.float32)
+    kids, k = [], 0
+    for nm in names:
+        m = len(ref_default_params(nm))
+        kids.append((nm, p[k:k + m]))
+        k += m
+    assert k == p.size, (key, p.size)
+    return ("Aggregate", kids)

@@ -67,6 +67,8 @@ def test_c_abi_parser_matches_reference_on_every_fit_line():
                 assert k == _lib.ERR_INVALID_ARG and b"float range" in lib.bbm_hip_last_error(), (fname, material)
                 continue
             assert k == 1 and lib.bbm_hip_model_name(ids[0]).decode() == key, (fname, material)
+            # every fit is Aggregate(Lambertian, X): the runtime aggregatebsdf of bsdf_import (bsdf_string_convert.h:59)
+            assert ids[0] & 0x40000000, (fname, material)
             assert np.array_equal(np.array(buf[:nps[0]], np.float32), np.asarray(params, np.float32)), (fname, material)
 
 

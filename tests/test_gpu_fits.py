@@ -1,8 +1,11 @@
 """Every published material on the GPU: each line of each fits/*.fit (1 302 fitted Aggregate(Lambertian, X)
 materials, tests/golden/fits.json) parsed by bbm_amd.fromString and evaluated on the golden direction set
 (1 024 hemisphere + 256 sphere pairs + 33 edge cases) through its fused kernel, against the reference itself
-(oracle/_ref: the reference's own aggregatemodel<lambertian, X> at those parameters) -- eval + pdf and
-reflectance, under the per-lane gate and proofs of tests/test_gpu_parity.py.  The golden fixtures pin 3-4
+(oracle/_ref: what the reference's bsdf_import builds from that line -- the runtime aggregatebsdf of bsdf_ptrs to
+lambertian and X at those parameters, oracle/ref_runtime.cpp) -- eval + pdf and reflectance, under the per-lane
+gate and proofs of tests/test_gpu_parity.py.  fromString gives the fused kernel the runtime aggregate's semantics
+(BBM_HIP_RUNTIME_AGGREGATE): its pdf adds w_k pdf_k / sum term by term where aggregatemodel divides the inner
+product.  The golden fixtures pin 3-4
 parameter sets per model; this is the parameter space the library is actually used with."""
 import json
 import os
@@ -43,15 +46,17 @@ def test_every_published_material_matches_reference(bbm, fname):
         assert m.name == key, (fname, mat)
         p = np.asarray(params, np.float32)
         np.testing.assert_array_equal(m.parameter_values(), p)
+        assert m.runtime, (fname, mat)
+        tree = ou.runtime_fit_tree(key, p)
         got = tp._gpu_evalpdf(m, pin, pout)
-        ref = ou.oracle_eval_pdf(key, p, pin, pout, nthreads=8)
-        provers = [tp._input_ulps_prover(lambda a, b: ou.oracle_eval_pdf(key, p, a, b, nthreads=8), [pin, pout], got),
-                   tp._libm_prover(lambda a, b: ou.oracle_eval_pdf(key, p, a, b, nthreads=1), [pin, pout], got)]
+        ref = ou.ref_runtime_eval_pdf(tree, pin, pout)
+        provers = [tp._input_ulps_prover(lambda a, b: ou.ref_runtime_eval_pdf(tree, a, b), [pin, pout], got),
+                   tp._libm_prover(lambda a, b: ou.ref_runtime_eval_pdf(tree, a, b, nthreads=1), [pin, pout], got)]
         st = tp.check_lanes(got, ref, f"{fname}:{mat} eval+pdf", provers, model=key)
         refl = m.reflectance(tp._dev(sout)).cpu().numpy()
-        rr = ou.ref_reflectance(key, p, sout)
+        rr = ou.ref_runtime_reflectance(tree, sout)
         tp.check_lanes(refl, rr, f"{fname}:{mat} reflectance",
-                       [tp._input_ulps_prover(lambda o: ou.ref_reflectance(key, p, o), [sout], refl)], model=key)
+                       [tp._input_ulps_prover(lambda o: ou.ref_runtime_reflectance(tree, o), [sout], refl)], model=key)
         stats[mat] = {k: st[k] for k in ("max_rel_normal", "max_rel_proven", "frac_bit_exact", "lanes_outside_bar",
                                          "proven_by")}
         n_mat += 1

@@ -27,8 +27,12 @@ def _tree(lib, s):
     return k, list(ids[:max(k, 0)]), list(nk[:max(k, 0)]), list(npar[:max(k, 0)]), buf
 
 
+RUNTIME = 0x40000000     # BBM_HIP_RUNTIME_AGGREGATE: a fused aggregate with aggregatebsdf semantics
+AGG_BSDF = -101          # BBM_HIP_AGGREGATE_BSDF: a composed runtime aggregate (aggregatebsdf.h)
+
+
 def _names(lib, ids):
-    return ["*" if i == -100 else lib.bbm_hip_model_name(i).decode() for i in ids]
+    return ["*" if i == AGG_BSDF else lib.bbm_hip_model_name(i).decode() for i in ids]
 
 
 needs_ref = pytest.mark.skipif(ou.ref() is None, reason="oracle/_ref not built")
@@ -45,19 +49,23 @@ def test_parse_tree_matches_reference_fromstring(bbm, key):
     assert k > 1
     want = ou.ref_from_string(key, s)
     assert np.array_equal(buf[:sum(npar)], want)        # the values the reference reads, leaves in preorder
-    assert ids[0] == -100 and nk[0] >= 2
+    assert ids[0] == AGG_BSDF and nk[0] >= 2
 
 
 def test_parse_tree_structure(bbm):
     lib = bbm._lib.load()
     k, ids, nk, npar, _ = _tree(lib, "Aggregate(Aggregate(Lambertian, Ward), GGX)")
     assert (k, _names(lib, ids), nk, npar) == (5, ["*", "*", "Lambertian", "Ward", "GGX"], [2, 2, 0, 0, 0], [0, 0, 3, 5, 5])
-    # a fused inner aggregate stays one registry entry
+    # a fused inner aggregate stays one registry entry -- the runtime aggregate of a string (bsdf_string_convert.h:59)
     k, ids, nk, npar, _ = _tree(lib, "Aggregate(Aggregate(Lambertian, CookTorrance), Ward)")
     assert (k, _names(lib, ids), nk) == (3, ["*", "Aggregate<Lambertian,CookTorrance>", "Ward"], [2, 0, 0])
+    assert ids[1] & RUNTIME and not ids[2] & RUNTIME
     # no composed aggregate: one node
     k, ids, nk, npar, _ = _tree(lib, "Aggregate(Lambertian, CookTorrance)")
     assert (k, _names(lib, ids), nk, npar) == (1, ["Aggregate<Lambertian,CookTorrance>"], [0], [8])
+    assert ids[0] & RUNTIME
+    # a runtime flag on a single model is not a model
+    assert lib.bbm_hip_model_name(lib.bbm_hip_model_id(b"Ward") | RUNTIME) is None
 
 
 def test_flat_parser_rejects_nested_composed_and_accepts_fused_children(bbm):
@@ -72,6 +80,7 @@ def test_flat_parser_rejects_nested_composed_and_accepts_fused_children(bbm):
     # a fused child is a registry entry like any other
     rc = lib.bbm_hip_parse_model(b"Aggregate(Aggregate(Lambertian, GGX), Ward)", ids, ptr, npar, 16, buf.size)
     assert rc == 2 and _names(lib, ids[:2]) == ["Aggregate<Lambertian,GGX>", "Ward"] and list(npar[:2]) == [8, 5]
+    assert ids[0] & RUNTIME
 
 
 def test_python_fromstring_nested(bbm):
