@@ -72,6 +72,14 @@ SIGNATURES = {
     "bbm_hip_scratch_trim_captured": (_SZ, []),
     "bbm_hip_scratch_bytes": (_SZ, []),
     "bbm_hip_libm_eval": (_I, [_I, _P, _P, _P, _SZ, _P]),
+    "bbm_hip_loss_tree_workspace_size": (_SZ, [_I, _SZ]),
+    "bbm_hip_loss_tree": (_I, [_P, _I, _P, _I, _I, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _U32, _U32, _P, _P, _SZ,
+                               _P]),
+    "bbm_hip_loss_tree_f64": (_I, [_P, _I, _P, _I, _I, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _U32, _U32, _P, _P,
+                                   _SZ, _P]),
+    "bbm_hip_check_tree_workspace_size": (_SZ, [_P]),
+    "bbm_hip_check_tree": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _P]),
+    "bbm_hip_check_tree_f64": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
 }
 
 ABI_VERSION = 10

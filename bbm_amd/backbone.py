@@ -528,6 +528,22 @@ class AggregateModel:
     def parameter_values(self, flag=None):
         return np.concatenate([c.parameter_values(flag) for c in self._children])
 
+    # the reference enumerates an aggregate's attributes child by child (bsdf_enumerate.h over the base classes)
+    def parameter_attrs(self):
+        return np.concatenate([c.parameter_attrs() for c in self._children])
+
+    def parameter_indices(self, flag=0x0F):
+        return np.nonzero(self.parameter_attrs() & np.uint32(flag))[0]
+
+    def parameter_default_values(self):
+        return np.concatenate([c.parameter_default_values() for c in self._children])
+
+    def parameter_lower_bound(self):
+        return np.concatenate([c.parameter_lower_bound() for c in self._children])
+
+    def parameter_upper_bound(self):
+        return np.concatenate([c.parameter_upper_bound() for c in self._children])
+
     def set_parameter_values(self, values):
         v = np.asarray(values, dtype=np.float32).reshape(-1)
         sizes = [c.parameter_values().size for c in self._children]
@@ -650,6 +666,21 @@ class AggregateModel:
         _lib.check(fn(desc, nd, ox, oy, oz, mptr, n, int(component), int(unit), rgb[0].data_ptr(),
                       rgb[1].data_ptr(), rgb[2].data_ptr(), _stream_ptr(stream)))
         return rgb
+
+
+def tree_desc(model, f64=False):
+    """Any model as a bbm_hip_child(_f64) tree for the *_tree entry points (bbm_hip_loss_tree, bbm_hip_check_tree):
+    (array, count, keep-alive list).  A single model (or fused aggregate, Merl) is one leaf node; an AggregateModel
+    its children or its runtime root node (AggregateModel._desc)."""
+    if isinstance(model, AggregateModel):
+        return model._desc(f64)
+    kind = _lib.ChildF64 if f64 else _lib.Child
+    arr = (kind * 1)()
+    p = model._pptr() if not f64 else None
+    params = np.ascontiguousarray(model._params, dtype=np.float64) if f64 else model._params
+    arr[0].model_id, arr[0].params, arr[0].nparams = model.model_id, params.ctypes.data, params.size
+    arr[0].children, arr[0].nchildren = None, 0
+    return arr, 1, [arr, params, p]
 
 
 def Aggregate(*children, fused=True, runtime=False):

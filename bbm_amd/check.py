@@ -26,7 +26,7 @@ import sys
 import numpy as np
 
 from . import _lib
-from .backbone import BsdfModel, _stream_ptr, _torch, fromString
+from .backbone import AggregateModel, BsdfModel, _stream_ptr, _torch, fromString, tree_desc
 
 REFLECTANCE, RECIPROCITY, ADJOINT, PDF, PDFINT, SAMPLE_PDF, SAMPLE_COUNT = range(7)
 ACC = 12
@@ -97,18 +97,24 @@ def _sum_counts(counts, dist):
 
 
 def run(model, test, samples, nslots=1, slot_dirs=None, seed=DEFAULT_SEED, sphere=False, importance=False,
-        include_zero=False, bins=(0, 0), begin=0, stream=None):
-    """One bbm_hip_check launch over samples [begin, begin + samples) of every slot on this GPU.
+        include_zero=False, bins=(0, 0), begin=0, stream=None, f64=False):
+    """One checkBsdf statistic over samples [begin, begin + samples) of every slot on this GPU: a single floatRGB
+    model through its fused reduction kernel (bbm_hip_check); any other model (composed / runtime aggregates) or
+    the doubleRGB configuration (f64) through the materialised path (bbm_hip_check_tree / _f64).
     Returns the (nslots, ACC) float64 accumulators, or for SAMPLE_COUNT the (nslots, bins) counts."""
     torch = _torch()
     lib = _lib.load()
     dev = torch.device("cuda", torch.cuda.current_device())
+    tree = bool(f64) or isinstance(model, AggregateModel)
     d = CheckDesc()
     d.test, d.nslots, d.seed, d.begin, d.n = int(test), int(nslots), int(seed), int(begin), int(samples)
     keep = None
+    sptr = (None, None, None)
     if slot_dirs is not None:
-        keep = slot_dirs.to(dev, torch.float32).contiguous()
-        d.slot_x, d.slot_y, d.slot_z = keep[0].data_ptr(), keep[1].data_ptr(), keep[2].data_ptr()
+        keep = slot_dirs.to(dev, torch.float64 if f64 else torch.float32).contiguous()
+        sptr = (keep[0].data_ptr(), keep[1].data_ptr(), keep[2].data_ptr())
+        if not f64:
+            d.slot_x, d.slot_y, d.slot_z = sptr
     d.sphere, d.importance, d.include_zero_pdf = int(bool(sphere)), int(bool(importance)), int(bool(include_zero))
     d.theta_bins, d.phi_bins = int(bins[0]), int(bins[1])
     nb = int(bins[0]) * int(bins[1])
@@ -119,11 +125,21 @@ def run(model, test, samples, nslots=1, slot_dirs=None, seed=DEFAULT_SEED, spher
     else:
         out = torch.empty((nslots, ACC), dtype=torch.float64, device=dev)
         acc_ptr, cnt_ptr = out.data_ptr(), None
-        wsb = int(lib.bbm_hip_check_workspace_size(ctypes.byref(d)))
+        wsf = lib.bbm_hip_check_tree_workspace_size if tree else lib.bbm_hip_check_workspace_size
+        wsb = int(wsf(ctypes.byref(d)))
         wst = torch.empty(max(wsb // 8, 1), dtype=torch.float64, device=dev)
         ws = wst.data_ptr()
-    _lib.check(lib.bbm_hip_check(model.model_id, model._pptr(), model._params.size, ctypes.byref(d), acc_ptr, cnt_ptr,
-                                 ws, wsb, _stream_ptr(stream)))
+    if tree:
+        desc, ndesc, _kd = tree_desc(model, bool(f64))
+        if f64:
+            _lib.check(lib.bbm_hip_check_tree_f64(desc, ndesc, ctypes.byref(d), sptr[0], sptr[1], sptr[2], acc_ptr,
+                                                  cnt_ptr, ws, wsb, _stream_ptr(stream)))
+        else:
+            _lib.check(lib.bbm_hip_check_tree(desc, ndesc, ctypes.byref(d), acc_ptr, cnt_ptr, ws, wsb,
+                                              _stream_ptr(stream)))
+    else:
+        _lib.check(lib.bbm_hip_check(model.model_id, model._pptr(), model._params.size, ctypes.byref(d), acc_ptr,
+                                     cnt_ptr, ws, wsb, _stream_ptr(stream)))
     res = out.cpu().numpy()
     del keep
     return res

@@ -532,10 +532,6 @@ __global__ __launch_bounds__(64) void k_check_final(const double* partial, int n
 namespace {
 
 // draw k of a check test: base key of the stream (test, k); the slot is mixed in by check_key
-uint64_t check_base_key(uint64_t seed, int test, int draw)
-{
-  return mix64(seed) ^ (0xd1b54a32d192ed03ull * (uint64_t(0x10000) * uint64_t(test + 1) + uint64_t(draw) + 1));
-}
 
 __global__ __launch_bounds__(kBlock) void k_draws(uint64_t key, uint64_t offset, uint64_t n, float* u0, float* u1)
 {

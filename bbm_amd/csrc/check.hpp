@@ -56,6 +56,12 @@ struct CheckArgs
   ParamBlock p;
 };
 
+// base key of draw `draw` (0..2 per sample, 3 = trial directions) of `test`
+__host__ __device__ __forceinline__ uint64_t check_base_key(uint64_t seed, int test, int draw)
+{
+  return mix64(seed) ^ (0xd1b54a32d192ed03ull * (uint64_t(0x10000) * uint64_t(test + 1) + uint64_t(draw) + 1));
+}
+
 // the key of draw k of slot s: streams never collide across slots, draws or tests
 __host__ __device__ __forceinline__ uint64_t check_key(uint64_t base, int slot) { return mix64(base + 0x2545f4914f6cdd1dull * uint64_t(slot)); }
 

@@ -197,4 +197,45 @@ __device__ __forceinline__ float sample_loss(int kind, const LossSample& s, cons
   }
 }
 
+// the same losses in doubleRGB (Value = double: every step of the reference's operator() in double; the log the
+// device's IEEE-accurate double log), for the materialised loss over any model tree (composite.hip)
+struct LossSampleD
+{
+  double c, sin_in, sin_out, cos_out;
+  double r[3], lr[3];
+};
+
+__device__ __forceinline__ LossSampleD loss_prepare_d(int kind, double inz, double outz, const double* ref)
+{
+  LossSampleD s;
+  s.c = fmax(inz, 0.0);
+  s.sin_in = sqrt(fmax(1 - inz * inz, 0.0));
+  s.sin_out = sqrt(fmax(1 - outz * outz, 0.0));
+  s.cos_out = fmax(outz, 0.0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+  {
+    s.r[k] = ref[k];
+    s.lr[k] = (kind >= kLossStandardLog) ? log(1 + ref[k] * s.c) : 0.0;
+  }
+  return s;
+}
+
+__device__ __forceinline__ double sample_loss_d(int kind, const LossSampleD& s, const double* v)
+{
+  double h = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+  {
+    const double e = (kind <= kLossBieronL2) ? (v[k] - s.r[k]) * s.c : log(1 + v[k] * s.c) - s.lr[k];
+    h = h + e * e;
+  }
+  switch (kind)
+  {
+    case kLossLowL2: case kLossLowLog: return h * s.sin_in;
+    case kLossBieronL2: case kLossBieronLog: return ((h * s.cos_out) * s.sin_in) * s.sin_out;
+    default: return (h * s.sin_in) * s.sin_out;
+  }
+}
+
 }  // namespace bbmhip

@@ -25,7 +25,7 @@ import math
 import numpy as np
 
 from . import _lib
-from .backbone import _on_stream, _stream_ptr, _torch
+from .backbone import AggregateModel, _on_stream, _stream_ptr, _torch, tree_desc
 
 LIN_SPHERICAL, LIN_MERL = 0, 1
 NGAN_L2, LOW_L2, BIERON_L2, STANDARD_LOG, LOW_LOG, BIERON_LOG = range(6)
@@ -104,25 +104,46 @@ def reference_table(model, lin, begin=0, n=None, stream=None):
 class SampledLoss:
     """sampledlossfunction<fitted, reference, loss, linearizer> (include/bbm/sampledlossfunction.h:34-97).
 
-    fitted: a BsdfModel whose parameter layout the probes use; reference: a BsdfModel (evaluated
-    once into a table on this rank's shard) or a (3, n_shard) CUDA tensor of reference values.
-    dist: torch.distributed module (or None); the shard is this rank's part of the grid."""
+    fitted: any model -- a BsdfModel (one fused kernel: bbm_hip_loss / bbm_hip_loss_pairs, all probes in one launch)
+    or an AggregateModel of any composition (composed aggregates and runtime aggregates: bbm_hip_loss_tree, the
+    probes evaluated through the children's kernels) -- whose parameter layout the probes use; reference: a model
+    (evaluated once into a table on this rank's shard) or a (3, n_shard) CUDA tensor of reference values.
+    f64: the doubleRGB configuration (bbm_hip_loss_tree_f64: directions, reference values, parameters and
+    per-sample losses in double).  dist: torch.distributed module (or None); the shard is this rank's part of the
+    grid."""
 
-    def __init__(self, fitted, reference, loss, lin, component=3, unit=0, dist=None, stream=None, materialize=True):
+    def __init__(self, fitted, reference, loss, lin=None, component=3, unit=0, dist=None, stream=None, materialize=True,
+                 f64=False, pairs=None):
         torch = _torch()
+        self.f64 = bool(f64)
+        # the fused multi-probe kernel serves single floatRGB models; everything else the materialised tree path
+        self.tree = self.f64 or isinstance(fitted, AggregateModel)
+        if self.tree:
+            materialize = True
+            if self.f64 and not fitted.has_f64():
+                raise _lib.BackboneError(_lib.ERR_UNSUPPORTED, f"{fitted.name}: no doubleRGB kernels")
         self.fitted = fitted
         self.loss_kind = LOSS_NAMES[loss] if isinstance(loss, str) else int(loss)
         self.lin = lin
         self.component, self.unit = int(component), int(unit)
         self.dist = dist
         self.stream = stream
-        self.total = lin.size()
-        rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
-        self.begin, end = shard_range(self.total, rank, world)
-        self.n = end - self.begin
-        # materialize: the shard's direction pairs are computed once (bbm_hip_linearize, 24 B/sample resident)
-        # and every compass step streams them (bbm_hip_loss_pairs) instead of recomputing the linearizer
-        self.pairs = lin.directions(self.begin, self.n, stream) if materialize else None
+        if pairs is not None:
+            # a table of direction pairs (this rank's own samples: the reference's sampledlossfunction over any
+            # linearizer, e.g. the measured directions of a material) instead of a grid
+            self.pairs = tuple(pairs)
+            self.n = self.total = int(self.pairs[0].shape[1])
+            self.begin = 0
+        else:
+            self.total = lin.size()
+            rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)
+            self.begin, end = shard_range(self.total, rank, world)
+            self.n = end - self.begin
+            # materialize: the shard's direction pairs are computed once (bbm_hip_linearize, 24 B/sample resident)
+            # and every compass step streams them (bbm_hip_loss_pairs) instead of recomputing the linearizer
+            self.pairs = lin.directions(self.begin, self.n, stream) if materialize else None
+        if self.f64:
+            self.pairs = tuple(d.double() for d in self.pairs)
         if hasattr(reference, "eval"):
             if self.pairs is not None:
                 self.ref = reference.eval(self.pairs[0], self.pairs[1], stream=stream)
@@ -130,6 +151,8 @@ class SampledLoss:
                 self.ref = reference_table(reference, lin, self.begin, self.n, stream)
         else:
             self.ref = reference
+        if self.f64:
+            self.ref = self.ref.double()
         if self.ref.shape != (3, self.n):
             raise ValueError(f"reference table: expected shape (3, {self.n}), got {tuple(self.ref.shape)}")
         self.dev = self.ref.device
@@ -143,7 +166,9 @@ class SampledLoss:
     def _workspace(self, nprobes):
         torch = _torch()
         if self._ws is None or self._ws_probes < nprobes:
-            nbytes = _lib.load().bbm_hip_loss_workspace_size(nprobes)
+            lib = _lib.load()
+            nbytes = (lib.bbm_hip_loss_tree_workspace_size(nprobes, self.n) if self.tree
+                      else lib.bbm_hip_loss_workspace_size(nprobes))
             self._ws = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=self.dev)
             self._ws_probes = nprobes
         return self._ws
@@ -161,8 +186,31 @@ class SampledLoss:
             self.dist.all_reduce(sums)
         return sums
 
+    def _tree_sums(self, probes):
+        """bbm_hip_loss_tree(_f64): any model, probes on the host."""
+        torch = _torch()
+        npar = self.fitted.parameter_values().size
+        p = np.ascontiguousarray(np.asarray(probes, dtype=np.float64 if self.f64 else np.float32).reshape(-1, npar))
+        nprobes = p.shape[0]
+        sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
+        ws = self._workspace(nprobes)
+        _on_stream(self.stream, sums, ws)
+        tree, ntree, _keep = tree_desc(self.fitted, self.f64)
+        lib = _lib.load()
+        fn = lib.bbm_hip_loss_tree_f64 if self.f64 else lib.bbm_hip_loss_tree
+        din, dout = self.pairs
+        _lib.check(fn(tree, ntree, p.ctypes.data, npar, nprobes, self.n, din[0].data_ptr(), din[1].data_ptr(),
+                      din[2].data_ptr(), dout[0].data_ptr(), dout[1].data_ptr(), dout[2].data_ptr(),
+                      self.ref[0].data_ptr(), self.ref[1].data_ptr(), self.ref[2].data_ptr(), self.loss_kind,
+                      self.component, self.unit, sums.data_ptr(), ws.data_ptr(), ws.numel() * 8,
+                      _stream_ptr(self.stream)))
+        self.launches += 1
+        return sums
+
     def local_sums(self, probes):
         """Per-probe loss sums over this rank's shard: one bbm_hip_loss launch -> float64 tensor (nprobes,)."""
+        if self.tree:
+            return self._tree_sums(probes)
         torch = _torch()
         p = np.ascontiguousarray(np.asarray(probes, dtype=np.float32).reshape(-1, self.fitted._params.size))
         nprobes, npar = p.shape
@@ -188,14 +236,16 @@ class SampledLoss:
         return sums
 
     def probe_losses(self, probes):
-        """Mean loss per probe (err / numsamples, sampledlossfunction.h:80-87) as float32 values."""
+        """Mean loss per probe (err / numsamples, sampledlossfunction.h:80-87) as Value: float32 values (float64 in
+        doubleRGB)."""
         s = self.probe_sums(probes).cpu().numpy()
-        return (s / float(self.total)).astype(np.float32)
+        return s / float(self.total) if getattr(self, "f64", False) else (s / float(self.total)).astype(np.float32)
 
     def __call__(self, params=None):
         """Loss of one parameter vector (the fitted model's current parameters by default)."""
-        p = self.fitted._params if params is None else params
-        return float(self.probe_losses(np.asarray(p, np.float32)[None])[0])
+        p = self.fitted.parameter_values() if params is None else params
+        f64 = getattr(self, "f64", False)
+        return float(self.probe_losses(np.asarray(p, np.float64 if f64 else np.float32)[None])[0])
 
 
 class Compass:
@@ -205,55 +255,68 @@ class Compass:
     fixed) inside [lower, upper] (default: the model's parameter bounds); the model's parameters
     are updated in place, like the reference's parameter references."""
 
-    def __init__(self, lossfunc, model=None, lower=None, upper=None, tolerance=EPSILON, step_size=1.0,
+    def __init__(self, lossfunc, model=None, lower=None, upper=None, tolerance=None, step_size=1.0,
                  contraction=0.5, expansion=1.0, flag=ALL):
         self.loss = lossfunc
         self.model = model if model is not None else lossfunc.fitted
+        # Value of the configuration: float32 (floatRGB) or float64 (the loss's doubleRGB), for every parameter,
+        # step and loss the compass holds (compass.h:40-60 is templated on the parameter type)
+        V = self.V = np.float64 if getattr(lossfunc, "f64", False) else _F32
         self.idx = self.model.parameter_indices(flag)
         full_lo = self.model.parameter_lower_bound()
         full_hi = self.model.parameter_upper_bound()
-        self.lower = (np.asarray(lower, _F32) if lower is not None else full_lo[self.idx]).astype(_F32)
-        self.upper = (np.asarray(upper, _F32) if upper is not None else full_hi[self.idx]).astype(_F32)
+        self.lower = (np.asarray(lower, V) if lower is not None else full_lo[self.idx]).astype(V)
+        self.upper = (np.asarray(upper, V) if upper is not None else full_hi[self.idx]).astype(V)
+        # the full parameter vector the probes are built from (the model keeps float storage; in doubleRGB the
+        # compass's double vector is the authoritative one, `parameters`)
+        self.full = np.asarray(self.model.parameter_values(), V).copy()
         self.directions = []
         for i in range(1, len(self.idx) + 1):       # for(Scalar i=1; i <= size(param); ++i) (compass.h:67-71)
             self.directions += [float(i), -float(i)]
-        self.initial_step = _F32(step_size)
-        self.tolerance = _F32(tolerance)
-        self.contraction, self.expansion = _F32(contraction), _F32(expansion)
+        eps = np.finfo(V).eps if tolerance is None else tolerance     # Constants::Epsilon() of the Value
+        self.initial_step = V(step_size)
+        self.tolerance = V(eps)
+        self.contraction, self.expansion = V(contraction), V(expansion)
         self.reset()
+
+    @property
+    def parameters(self):
+        """The current full parameter vector in the configuration's Value type."""
+        return self.full.copy()
 
     def reset(self):
         """compass.h:145-150: step size back to the initial one, loss of the current parameters."""
         self.step_size = self.initial_step
-        self.loss_value = _F32(self.loss(self.model._params))
+        self.loss_value = self.V(self.loss(self.full))
 
     def is_converged(self):
         return bool(self.step_size < self.tolerance)
 
     def _params(self):
-        return self.model._params[self.idx].astype(_F32)
+        return self.full[self.idx].astype(self.V)
 
     def step(self):
         """One compass step (compass.h:82-140).  Returns the loss after the update."""
+        V = self.V
         if self.is_converged():
-            return _F32(0)
+            return V(0)
         param = self._params()
         s = self.step_size
         probes, in_box = [], []
-        full = self.model._params.copy()
+        full = self.full.copy()
         for card in self.directions:
             k = int(abs(card)) - 1
-            # probe(cardinal): value = param[k] + (cardinal < 0 ? -step : step), float arithmetic
-            param[k] = _F32(param[k] + (-s if card < 0 else s))
+            # probe(cardinal): value = param[k] + (cardinal < 0 ? -step : step), Value arithmetic
+            param[k] = V(param[k] + (-s if card < 0 else s))
             inb = bool(np.all((param >= self.lower) & (param <= self.upper)))
             full[self.idx] = param
             probes.append(full.copy())
             in_box.append(inb)
             # probe(-cardinal): the reference restores by the opposite update (not by assignment)
-            param[k] = _F32(param[k] + (s if card < 0 else -s))
+            param[k] = V(param[k] + (s if card < 0 else -s))
         probes = np.stack(probes)
         in_box = np.asarray(in_box)
-        errs = np.zeros(len(probes), _F32)
+        errs = np.zeros(len(probes), V)
         if in_box.any():
             errs[in_box] = self.loss.probe_losses(probes[in_box])
         # sequential selection of the strictly best in-box probe (compass.h:118-121)
@@ -264,10 +327,11 @@ class Compass:
         optimize = bool(loss < self.loss_value)
         if optimize and best != 0:
             k = int(abs(best)) - 1
-            param[k] = _F32(param[k] + (-s if best < 0 else s))
+            param[k] = V(param[k] + (-s if best < 0 else s))
         # the parameters keep any round-off of the probe/restore sequence, as the reference's do
-        self.model._params[self.idx] = param
-        self.step_size = _F32(self.expansion * s) if optimize else _F32(self.contraction * s)
+        self.full[self.idx] = param
+        self.model.set_parameter_values(self.full)
+        self.step_size = V(self.expansion * s) if optimize else V(self.contraction * s)
         if optimize:
-            self.loss_value = _F32(loss)
+            self.loss_value = V(loss)
         return self.loss_value

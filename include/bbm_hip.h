@@ -329,6 +329,29 @@ int bbm_hip_loss_pairs(int model_id, const float* probes, int nparams, int nprob
                        int loss_kind, uint32_t component, uint32_t unit,
                        double* sums, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The fitting loss of ANY model -- a single registry model, a fused or composed aggregate of either kind, nested to
+ * any depth -- in floatRGB or doubleRGB (sampledlossfunction<BSDF, ...> takes any bsdfmodel and any configuration,
+ * include/bbm/sampledlossfunction.h:34, :62-87), over n caller-provided pairs as bbm_hip_loss_pairs.  The model is a
+ * child tree (bbm_hip_aggregate_*: a single model is one leaf node, ntree = 1) whose structure is used and whose
+ * leaves' parameters are replaced, probe by probe, by the probe vectors: probes are HOST memory, nprobes x nparams
+ * values, each the leaves' parameter vectors back to back in preorder.  Every probe is evaluated through the
+ * model's kernels (composed aggregates: one pass per child) into device scratch and reduced per workgroup; sums as
+ * bbm_hip_loss (device, nprobes doubles; f64: the per-sample losses in double throughout).  Workspace:
+ * bbm_hip_loss_tree_workspace_size(nprobes, n) bytes of device memory. */
+size_t bbm_hip_loss_tree_workspace_size(int nprobes, size_t n);
+int bbm_hip_loss_tree(const bbm_hip_child* tree, int ntree, const float* probes, int nparams, int nprobes, size_t n,
+                      const float* in_x, const float* in_y, const float* in_z,
+                      const float* out_x, const float* out_y, const float* out_z,
+                      const float* ref_r, const float* ref_g, const float* ref_b,
+                      int loss_kind, uint32_t component, uint32_t unit,
+                      double* sums, void* workspace, size_t workspace_bytes, void* stream);
+int bbm_hip_loss_tree_f64(const bbm_hip_child_f64* tree, int ntree, const double* probes, int nparams, int nprobes,
+                          size_t n, const double* in_x, const double* in_y, const double* in_z,
+                          const double* out_x, const double* out_y, const double* out_z,
+                          const double* ref_r, const double* ref_g, const double* ref_b,
+                          int loss_kind, uint32_t component, uint32_t unit,
+                          double* sums, void* workspace, size_t workspace_bytes, void* stream);
+
 /* The EPD model's shadowing table G1[p][t] (100 x 1000 floats, row-major; the reference's
  * include/precomputed/holzschuchpacanowski/G1.h), built on the current device on first use by
  * restating its generator (precompute/HolzschuchPacanowski/G1.cpp).  Copies min(capacity, 100000)
@@ -405,6 +428,20 @@ size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* desc);
 /* Run one checkBsdf statistic of model_id (params uniform) -> acc / counts (device). */
 int bbm_hip_check(int model_id, const float* params, int nparams, const bbm_hip_check_desc* desc,
                   double* acc, uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+
+/* checkBsdf for ANY model (a child tree as in bbm_hip_loss_tree, leaves with their own parameters; checkBsdf builds
+ * any model string through bsdf_import, bin/checkBsdf.cpp:435-479) and for doubleRGB.  The same tests, draws, slot
+ * semantics, accumulator layout and fixed-order final reduction as bbm_hip_check; the per-sample quantities are
+ * materialised in chunks through the model's own sample / eval / pdf entry points (composed aggregates: one pass per
+ * child) and reduced per chunk.  f64: every per-sample quantity in double (sampleSphere, the chi-square points and
+ * bins in double), the slot directions given as doubles (the descriptor's float slot pointers are ignored).
+ * Workspace: bbm_hip_check_tree_workspace_size(desc) bytes of device memory (0 for SAMPLE_COUNT). */
+size_t bbm_hip_check_tree_workspace_size(const bbm_hip_check_desc* desc);
+int bbm_hip_check_tree(const bbm_hip_child* tree, int ntree, const bbm_hip_check_desc* desc, double* acc,
+                       uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+int bbm_hip_check_tree_f64(const bbm_hip_child_f64* tree, int ntree, const bbm_hip_check_desc* desc,
+                           const double* slot_x, const double* slot_y, const double* slot_z, double* acc,
+                           uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
 
 /* The uniforms draw `draw` (0..2) of slot `slot` of `test` uses for samples offset .. offset + n - 1
  * (rndVec2d(), checkBsdf.cpp:21-26): xi0[i], xi1[i] in [0, 1), 24-bit. */

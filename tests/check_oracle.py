@@ -97,7 +97,17 @@ def _bcast(v, n):
 
 
 def _eval(name, params, din, dout):
+    """eval + pdf of the reference model `name` at `params`; name may also be a runtime-aggregate tree
+    (oracle_util.runtime_tree form: the reference's own aggregatebsdf of bsdf_ptrs), params then unused."""
+    if isinstance(name, tuple):
+        return ou.ref_runtime_eval_pdf(name, din, dout)
     return ou.ref_eval_pdf(name, params, din, dout, nthreads=8)
+
+
+def _sample(name, params, out, xi):
+    if isinstance(name, tuple):
+        return ou.ref_runtime_sample(name, out, xi)
+    return ou.ref_sample(name, params, out, xi, nthreads=8)
 
 
 def reflectance(name, params, out, samples, seed, slot, importance, begin=0):
@@ -105,7 +115,7 @@ def reflectance(name, params, out, samples, seed, slot, importance, begin=0):
     xi = draws(REFLECTANCE, seed, slot, 0, begin, samples)
     outs = _bcast(out, samples)
     if importance:
-        s, _ = ou.ref_sample(name, params, outs, xi, nthreads=8)
+        s, _ = _sample(name, params, outs, xi)
         d, pdf = s[:3], s[3]
     else:
         d, pdf = sphere_dirs(xi)
@@ -134,7 +144,7 @@ def pdf_test(name, params, samples, seed, sphere, begin=0):
     out, _ = sphere_dirs(draws(PDF, seed, 0, 0, begin, samples), hemisphere=not sphere)
     res = []
     for draw in (1, 2):
-        s, _ = ou.ref_sample(name, params, out, draws(PDF, seed, 0, draw, begin, samples), nthreads=8)
+        s, _ = _sample(name, params, out, draws(PDF, seed, 0, draw, begin, samples))
         p = _eval(name, params, s[:3], out)[3]
         res.append((int((p < 0).sum()), int((s[2] < 0).sum()), float(np.abs(s[3] - p).sum(dtype=np.float64))))
     return res
@@ -162,7 +172,7 @@ def sample_pdf(name, params, t, trial, bins, pdf_samples, seed, theta, phi):
 def sample_count(name, params, t, trial, samples, seed, theta, phi, include_zero=False):
     """checkBsdf.cpp:360-380: histogram of sampled directions over the (theta x phi) bins."""
     xi = draws(SAMPLE_COUNT, seed, trial, 0, 0, samples)
-    s, _ = ou.ref_sample(name, params, _bcast(t, samples), xi, nthreads=8)
+    s, _ = _sample(name, params, _bcast(t, samples), xi)
     ok = np.ones(samples, bool) if include_zero else (s[3] > EPS)
     idx = chi2_bins(s[:3, ok], theta, phi)
     return np.bincount(idx.astype(np.int64), minlength=theta * phi)
