@@ -10,12 +10,13 @@ Importing the package loads the HIP library; if it is missing the import fails l
 """
 from . import _lib
 from .backbone import (Aggregate, AggregateModel, BsdfModel, BsdfSample, bsdf_flag, bsdf_import, fill_directions, fromString,
-                       model_names, scratch_bytes, scratch_trim, scratch_trim_captured, set_exact_subnormals, unit_t, _make_ctor)
+                       parse_model, model_names, scratch_bytes, scratch_trim, scratch_trim_captured, set_exact_subnormals, unit_t, _make_ctor)
 from .models import ATTRIBUTES
 
 _lib.load()
 
-__all__ = ["Aggregate", "AggregateModel", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import", "model_names",
+__all__ = ["Aggregate", "AggregateModel", "BsdfModel", "BsdfSample", "bsdf_flag", "unit_t", "fromString", "bsdf_import",
+           "parse_model", "model_names",
            "fill_directions", "scratch_trim", "scratch_trim_captured", "scratch_bytes", "set_exact_subnormals", "ATTRIBUTES"]
 
 from .merl import Merl  # noqa: E402  -- measured data: constructed from a file, not from attributes

@@ -489,6 +489,35 @@ def fromString(s):
 bsdf_import = fromString
 
 
+def parse_model(s):
+    """fromString through the library's own C-ABI parser (bbm_hip_parse_model_tree, the restatement of the
+    reference's runtime fromString, bsdf_string_convert.h:52-85, that FFI callers use): the same models as
+    fromString, built from the parser's preorder tree -- registry leaves (a fused runtime aggregate keeps its
+    BBM_HIP_RUNTIME_AGGREGATE id), BBM_HIP_AGGREGATE_BSDF nodes as runtime AggregateModels."""
+    lib = _lib.load()
+    cap_nodes, cap_params = 256, 1 << 14
+    ids, nk, npar = (ctypes.c_int * cap_nodes)(), (ctypes.c_int * cap_nodes)(), (ctypes.c_int * cap_nodes)()
+    buf = np.zeros(cap_params, np.float32)
+    k = _lib.check(lib.bbm_hip_parse_model_tree(s.encode(), ids, nk, buf.ctypes.data_as(ctypes.c_void_p), npar,
+                                                 cap_nodes, cap_params))
+    pos = [0, 0]            # next node, next parameter
+
+    def build():
+        i = pos[0]
+        pos[0] += 1
+        if ids[i] == _lib.AGGREGATE_BSDF:
+            return AggregateModel(*[build() for _ in range(nk[i])], runtime=True)
+        mid = ids[i]
+        m = BsdfModel(lib.bbm_hip_model_name(mid & ~_lib.RUNTIME_AGGREGATE).decode())
+        m.set_parameter_values(buf[pos[1]:pos[1] + npar[i]])
+        pos[1] += npar[i]
+        m.model_id = mid
+        return m
+    m = build()
+    assert pos[0] == k
+    return m
+
+
 def _copy_model(m):
     """A copy of a model for an aggregate (aggregatemodel_base copies its children, aggregatemodel.h:34): same
     class, own parameter vector, and every other attribute shared -- a Merl child keeps the reference to the

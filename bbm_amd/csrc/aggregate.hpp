@@ -34,6 +34,20 @@ struct Aggregate
   bool runtime;            // aggregatebsdf (fromString / bsdf_ptr) rather than aggregatemodel semantics
   __device__ explicit Aggregate(const float* p) : a(p), b(p + A::kParams), runtime(p[kAggregateModeSlot] != 0.0f) {}
 
+  // both children's per-pair preludes (the loss kernel): eval_geo is eval's rgb = e_A + e_B from them
+  static constexpr bool kHasGeo = has_geo<A>() && has_geo<B>();
+  struct Geo { typename A::Geo a; typename B::Geo b; };
+  __device__ __forceinline__ static Geo geometry(v3 in, v3 out) { return Geo{A::geometry(in, out), B::geometry(in, out)}; }
+  __device__ __forceinline__ void eval_geo(Geo& g, uint32_t component, float* rgb) const
+  {
+    float ra[3], rb[3];
+    a.eval_geo(g.a, component, ra);
+    b.eval_geo(g.b, component, rb);
+    rgb[0] = ra[0] + rb[0];
+    rgb[1] = ra[1] + rb[1];
+    rgb[2] = ra[2] + rb[2];
+  }
+
   // hsum(reflectance(out)) per child: std::accumulate from Value(0) (horizontal.h:64-67)
   __device__ __forceinline__ void weights(v3 out, uint32_t component, float& wa, float& wb) const
   {

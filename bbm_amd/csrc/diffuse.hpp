@@ -8,10 +8,20 @@ namespace bbmhip {
 // bbm::lambertian (include/bsdfmodel/lambertian.h:22-153); params: albedo RGB.
 struct Lambertian
 {
+  static constexpr bool kHasGeo = true;
   static constexpr int kParams = 3;
   static constexpr uint32_t kComponent = kFlagDiffuse;
   float albedo[3];
   __device__ explicit Lambertian(const float* p) { albedo[0] = p[0]; albedo[1] = p[1]; albedo[2] = p[2]; }
+
+  // the loss kernel's per-pair prelude (kernels.hpp k_loss): nothing to share beyond the pair itself
+  struct Geo { v3 in, out; };
+  __device__ __forceinline__ static Geo geometry(v3 in, v3 out) { return Geo{in, out}; }
+  __device__ __forceinline__ void eval_geo(const Geo& g, uint32_t component, float* rgb) const
+  {
+    float pdf;
+    eval_pdf<kModeEval>(g.in, g.out, component, rgb, pdf);
+  }
 
   // lambertian.h:45-59 eval (albedo * InvPi, non-strict z >= 0) and :115-125 pdf (z_in * InvPi)
   template<int MODE>

@@ -845,14 +845,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_wav
       else lin_pair(a.lin, a.begin + i, in, out);
       const float ref[3] = {a.ref_r[i], a.ref_g[i], a.ref_b[i]};
       const LossSample s = loss_prepare(a.loss_kind, in, out, ref);
-#pragma unroll
-      for (int j = 0; j < kProbeBatch; ++j)
+      if constexpr (has_geo<Model>())
       {
-        if (p0 + j >= a.nprobes) break;           // uniform
-        const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(p0 + j) * kLossModelBytes);
-        float rgb[3], pdf;
-        m.template eval_pdf<kModeEval>(in, out, a.component, rgb, pdf);
-        acc[j] += double(sample_loss(a.loss_kind, s, rgb));
+        // the parameter-independent prelude (halfway vector, masks, ...) once per pair for all the batch's probes
+        typename Model::Geo geo = Model::geometry(in, out);
+#pragma unroll
+        for (int j = 0; j < kProbeBatch; ++j)
+        {
+          if (p0 + j >= a.nprobes) break;           // uniform
+          const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(p0 + j) * kLossModelBytes);
+          float rgb[3];
+          m.eval_geo(geo, a.component, rgb);
+          acc[j] += double(sample_loss(a.loss_kind, s, rgb));
+        }
+      }
+      else
+      {
+#pragma unroll
+        for (int j = 0; j < kProbeBatch; ++j)
+        {
+          if (p0 + j >= a.nprobes) break;           // uniform
+          const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(p0 + j) * kLossModelBytes);
+          float rgb[3], pdf;
+          m.template eval_pdf<kModeEval>(in, out, a.component, rgb, pdf);
+          acc[j] += double(sample_loss(a.loss_kind, s, rgb));
+        }
       }
     }
 #pragma unroll

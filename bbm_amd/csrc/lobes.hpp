@@ -30,7 +30,10 @@ __device__ __forceinline__ v3 reflect_about(v3 out, v3 m)
 // toGlobalShadingFrame(normal) * v (core/shading_frame.h:24-48, Duff et al. 2017): columns X, Y, Z
 __device__ __forceinline__ v3 to_global(v3 normal, v3 v)
 {
-  const v3 Z = normalize3(normal);
+  // the normal is a model parameter (any vector a caller sets): the IEEE-style quotient keeps the reference's
+  // results at the edges (|n|^2 = inf -> 0 components, not NaN); directions use the fast normalize3
+  const float rn = div_nr(1.0f, sqrtf(dot3(normal, normal)));
+  const v3 Z = mk3(normal.x * rn, normal.y * rn, normal.z * rn);
   const float sign = copysignf(1.0f, Z.z);
   const float a = div_nr(-1.0f, sign + Z.z);          // -1.0 / (sign + z): one double op on floats
   const float b = Z.x * Z.y * a;
@@ -113,7 +116,7 @@ struct Ward
     const float cx = c * rx, cy = s * ry;
     const float r = div_nr(1.0f, sqrtf(sqnorm2(cx, cy)));
     const float csx = cx * r, csy = cy * r;
-    const float cosT = float(1.0 / sqrt(1.0 - double(div_nr(logf(xi1), sqnorm2(div_nr(csx, rx), div_nr(csy, ry))))));
+    const float cosT = float(1.0 / sqrt(1.0 - double(div_nr(logf_glibc(xi1), sqnorm2(div_nr(csx, rx), div_nr(csy, ry))))));
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
     dir = reflect_about(out, mk3(csx * sinT, csy * sinT, cosT));
     float rgb[3];
@@ -476,7 +479,7 @@ struct LowSmooth
     const float ro2 = sin_theta2(out);
     const double t = 1.0 + (2 * B * (1.0 + ro2)) + pow2d(B * (1.0 - ro2));
     const float temp_f = float(t);
-    const float temp = -logf(2.0f) + logf(1 + B * (1 - ro2) + safe_sqrtf(temp_f));
+    const float temp = -logf_glibc(2.0f) + logf_glibc(1 + B * (1 - ro2) + safe_sqrtf(temp_f));   // float logs (glibc)
     return B * kInvPiF * div_nr(1.0f, temp);
   }
   __device__ __forceinline__ static double pow2d(double x) { return x * x; }

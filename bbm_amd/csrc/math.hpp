@@ -43,6 +43,14 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 struct v3 { float x, y, z; };
 struct v2 { float x, y; };
 
+// a model policy with a parameter-independent per-pair prelude: geometry(in, out) / eval_geo(geo, ...) (Bagher,
+// Lambertian, their aggregates), which the fitting-loss kernel shares across the probes it evaluates at a pair
+template<class M> constexpr bool has_geo()
+{
+  if constexpr (requires { M::kHasGeo; }) return M::kHasGeo;
+  else return false;
+}
+
 __device__ __forceinline__ v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
 
@@ -601,6 +609,27 @@ __device__ __forceinline__ double ddiv_nr(double n, double d)
   const double rem = __builtin_fma(-d, q, n);
   const double q1 = __builtin_fma(rem, r, q);
   return __builtin_isfinite(q1) ? q1 : n * __builtin_amdgcn_rcp(d);
+}
+
+// float(1.0 + sqrt(x)) for a double x >= 1, every step IEEE double as in the reference (ggx.h:180-185's
+// 1 + sqrt(1 + alpha^2 tan^2) stored into a float `Value denom`), without the ~11 f64 VALU of the IEEE double
+// square root: a float rsq seed (|rel. error| <= 2^-22.2 with the rounding of x to float) and one double Newton step
+// give y = sqrt(x) within 2^-43.4 y, so 1 + y lands within ~800 double ulps of the reference's double.  Its float
+// rounding can only differ where that double is that close to a float rounding midpoint (the low 29 bits near
+// 2^28): those lanes (~1 in 2^16), and any x outside [1, 2^100], run the exact sequence instead -- the float is
+// always the reference's.  Pinned against IEEE double on the host by tests/test_gpu_libm.py.
+__device__ __forceinline__ float f_one_plus_sqrt(double x)
+{
+  const float xf = float(x);
+  const float g = __builtin_amdgcn_rsqf(xf);
+  const double s = double(xf * g);
+  const double y = __builtin_fma(__builtin_fma(-s, s, x), double(0.5f * g), s);
+  const double z = 1.0 + y;
+  const uint32_t lo = uint32_t(__builtin_bit_cast(uint64_t, z)) & 0x1fffffffu;
+  float res = float(z);
+  if (__builtin_expect(((lo - 0x0ffff000u) < 0x2000u) || !(x >= 1.0 && x <= 0x1p100), false))
+    res = float(1.0 + __builtin_sqrt(x));
+  return res;
 }
 
 // float(n / d) for double n, d -- the reference's double-promoted quotients that are immediately

@@ -121,7 +121,7 @@ struct GGX
   {
     const bool mask = (v.z > 0) && (dot3(v, m) > 0);
     const float r2 = (1.0f * au) * av;
-    const float denom = float(1.0 + sqrt(1.0 + r2 * tan_theta2(v)));
+    const float denom = f_one_plus_sqrt(1.0 + r2 * tan_theta2(v));      // float(1.0 + sqrt(...)), math.hpp
     // 2.0 / denom rounded to float: one IEEE op on float operands evaluated in double and rounded
     // once more to float is the float op itself (53 >= 2*24+2: double rounding is innocuous)
     return mask ? div_nr(2.0f, denom) : 0.0f;
@@ -434,8 +434,11 @@ struct FresnelCook
   __device__ __forceinline__ float eval(float c) const
   {
     const float g = safe_sqrtf(eta * eta + c * c - 1.0f);
-    // c = (in.h + out.h) / 2 > 0 where the result is used, g >= 0, and for eta >= 1 (its lower bound) g - c =
-    // (eta^2 - 1) / (g + c) >= 0: both denominators are normal and positive, both quotients normal or 0
+    // c = (in.h + out.h) / 2 in (0, 1] where the result is used and g >= 0, for ANY eta (the attribute's bound
+    // eta >= 1, bsdf_attribute.h:89, is metadata the reference does not enforce): g + c >= c is a positive normal
+    // float, and c (g - c) + 1 is either 0 (only at eta = 0 with c = 1, where the numerator is 0 as well: NaN in
+    // both) or >= 2^-24 (1 - c^2 near 1 is a multiple of float steps); both quotients are normal, 0 or that NaN,
+    // where the Markstein step alone (div_nr_n) is the IEEE quotient
     const float a = div_nr_n(g - c, g + c);
     const float b = div_nr_n(c * (g + c) - 1.0f, c * (g - c) + 1.0f);
     return fmaxf(0.5f * (a * a) * (1.0f + b * b), 0.0f);   // bbm::max(x, 0.0): fmax in double == fmaxf here

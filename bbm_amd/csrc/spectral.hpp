@@ -32,6 +32,7 @@ __device__ __forceinline__ float theta_of(v3 v)
 
 struct Bagher
 {
+  static constexpr bool kHasGeo = true;      // geometry() / eval_geo(): the loss kernel shares the prelude per pair
   static constexpr int kParams = 30;
   static constexpr uint32_t kComponent = kFlagSpecular;
   float albedo[3], K[3], Lambda[3], c[3], theta0[3], k[3], alpha[3], p[3], F0[3], F1[3];
@@ -81,52 +82,85 @@ struct Bagher
     return g;
   }
 
+  // The parameter-independent part of eval (the halfway vector, its tan^2, cos^4 pi, the masks, the chords and
+  // the Schlick base), computed once per direction pair and shared by every parameter vector evaluated at it (the
+  // fitting loss evaluates 2P probes per pair, kernels.hpp k_loss).  theta(in) / theta(out) are filled on first
+  // need (th < 0: not yet), since only lanes beyond a probe's theta0 use them.
+  struct Geo
+  {
+    v3 in, out, h;
+    float outh, tan2, q_in, q_out, th_in, th_out, cosF, zz;
+    double dnorm, x5;
+    bool sdirs, gmask;
+  };
+
+  __device__ __forceinline__ static Geo geometry(v3 in, v3 out)
+  {
+    Geo g;
+    g.in = in;
+    g.out = out;
+    g.sdirs = (in.z > 0.0f) && (out.z > 0.0f);
+    g.h = halfway(in, out);
+    g.outh = dot3(out, g.h);
+    const float inh = dot3(in, g.h);
+    g.tan2 = tan_theta2(g.h);
+    const double z2 = double(g.h.z) * double(g.h.z);
+    g.dnorm = double(kPiF) * (z2 * z2);      // Constants::Pi() * pow(cos, 4.0) (sgd.h:62)
+    // uncorrelated (uncorrelated.h:30-42) + sgd::G1 masks: z(v) > 0 and v.m > 0 for both
+    g.gmask = (inh > 0) && (g.outh > 0);
+    g.q_in = chord2(in);
+    g.q_out = chord2(out);
+    g.th_in = g.th_out = -1.0f;
+    g.cosF = 0.5f * (inh + g.outh);
+    const double x = double(1.0f - g.cosF);
+    g.x5 = (x * x) * (x * x) * x;
+    g.zz = in.z * out.z;
+    return g;
+  }
+
+  // eval (Specular component) at a prepared pair
+  __device__ __forceinline__ void eval_geo(Geo& g, uint32_t component, float* rgb) const
+  {
+    const bool active = (component & kFlagSpecular) && g.sdirs;
+    // in.z, out.z > 0 on every lane whose result is used: theta_of only where a channel may need it
+    if (g.q_in > qc_min && g.th_in < 0.0f) g.th_in = theta_of(g.in);
+    if (g.q_out > qc_min && g.th_out < 0.0f) g.th_out = theta_of(g.out);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+    {
+      // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
+      const float t = alpha[j] + div_nr(g.tan2, alpha[j]);
+      // exp(-t) / t^p: powf_fast (~1e-6) instead of the 173-instruction library powf.  Next to that factor the
+      // glibc-exact expf buys nothing (bit-exact lanes 68.9 -> 69.7 %) and cost 12 % (0.162 -> 0.183 ms per
+      // 10 M pairs, tools/gpu_r03_e.sh): expf_dn here
+#ifdef BBM_HIP_BAGHER_EXACT_D
+      const float den = powf_glibc(t, p[j]);
+      const float P22 = (den > kEpsF) ? div_nr(expf_glibc_neg(-t), den) : 0.0f;
+#else
+      const float den = powf_fast(t, p[j]);
+      const float P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
+#endif
+      const float Dj = ((g.h.z > 0) ? f_div_d(double(P22), g.dnorm) : 0.0f) * K[j];
+      const float Gj = g.gmask ? G1q(j, g.q_in, g.th_in) * G1q(j, g.q_out, g.th_out) : 0.0f;
+      // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
+      const float S = float(double(F0[j]) + double(1.0f - F0[j]) * g.x5);
+      const float Fj = S - F1[j] * g.cosF;
+      const float res = eval_scale<Norm::Cook>((Dj * Gj) * Fj, g.zz);
+      rgb[j] = active ? res * albedo[j] : 0.0f;
+    }
+  }
+
   template<int MODE>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
-    const bool active = (component & kFlagSpecular) && (in.z > 0.0f) && (out.z > 0.0f);
-    const v3 h = halfway(in, out);
-    const float outh = dot3(out, h);
-    if (MODE & kModeEval)
-    {
-      const float inh = dot3(in, h);
-      const float tan2 = tan_theta2(h);
-      const double z2 = double(h.z) * double(h.z);
-      const double dnorm = double(kPiF) * (z2 * z2);      // Constants::Pi() * pow(cos, 4.0) (sgd.h:62)
-      // uncorrelated (uncorrelated.h:30-42) + sgd::G1 masks: z(v) > 0 and v.m > 0 for both
-      const bool gmask = (inh > 0) && (outh > 0);
-      // in.z, out.z > 0 on every lane whose result is used: theta_of only where a channel may need it
-      const float q_in = chord2(in), q_out = chord2(out);
-      float th_in = 0.0f, th_out = 0.0f;
-      if (q_in > qc_min) th_in = theta_of(in);
-      if (q_out > qc_min) th_out = theta_of(out);
-      const float cosF = 0.5f * (inh + outh);
-      const double x = double(1.0f - cosF);
-      const double x5 = (x * x) * (x * x) * x;
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-      {
-        // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
-        const float t = alpha[j] + div_nr(tan2, alpha[j]);
-        // exp(-t) / t^p: powf_fast (~1e-6) instead of the 173-instruction library powf.  Next to that factor the
-        // glibc-exact expf buys nothing (bit-exact lanes 68.9 -> 69.7 %) and cost 12 % (0.162 -> 0.183 ms per
-        // 10 M pairs, tools/gpu_r03_e.sh): expf_dn here
-        const float den = powf_fast(t, p[j]);
-        const float P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
-        const float Dj = ((h.z > 0) ? f_div_d(double(P22), dnorm) : 0.0f) * K[j];
-        const float Gj = gmask ? G1q(j, q_in, th_in) * G1q(j, q_out, th_out) : 0.0f;
-        // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
-        const float S = float(double(F0[j]) + double(1.0f - F0[j]) * x5);
-        const float Fj = S - F1[j] * cosF;
-        const float res = eval_scale<Norm::Cook>((Dj * Gj) * Fj, in.z * out.z);
-        rgb[j] = active ? res * albedo[j] : 0.0f;
-      }
-    }
+    Geo g = geometry(in, out);
+    if (MODE & kModeEval) eval_geo(g, component, rgb);
     else rgb[0] = rgb[1] = rgb[2] = 0.0f;
     if (MODE & kModePdf)
     {
-      const float Dg = ggx.eval(h);
-      const float pp = div_nr(ggx.pdf(out, h, Dg), 4.0f * fabsf(outh));
+      const bool active = (component & kFlagSpecular) && g.sdirs;
+      const float Dg = ggx.eval(g.h);
+      const float pp = div_nr(ggx.pdf(out, g.h, Dg), 4.0f * fabsf(g.outh));
       pdf = active ? pp : 0.0f;
     }
     else pdf = 0.0f;

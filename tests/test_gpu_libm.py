@@ -13,7 +13,7 @@ from tests import oracle_util as ou
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4}
+FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4, "one_plus_sqrt": 5}
 
 
 @pytest.fixture(scope="module")
@@ -81,3 +81,21 @@ def test_powf_bitexact(lib):
     got, want = _device(lib, "powf", a, b), _host("powf", a, b)
     bad = np.nonzero(~_same(got, want))[0]
     assert bad.size == 0, f"powf: {bad.size} lanes differ, e.g. x={a[bad[:4]]} y={b[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"
+
+
+def test_one_plus_sqrt_bitexact(lib):
+    """math.hpp f_one_plus_sqrt (the GGX G1 denominator float(1.0 + sqrt(1.0 + alpha^2 tan^2)), ggx.h:180-185) against
+    the same IEEE double steps in numpy: a float rsq seed + one Newton step, with the exact sequence on lanes near a
+    float rounding midpoint -- so every lane must be bit-identical, including those the fallback takes."""
+    rng = np.random.default_rng(20261018)
+    n = 1 << 22
+    a = np.concatenate([rng.uniform(1e-4, 4, n).astype(np.float32),                 # alpha^2 (roughness^2 products)
+                        np.ones(n, np.float32),
+                        np.array([0, 1, 2, 3.5, 1e-30, 1e30, 1e30, np.inf, 1], np.float32)])
+    b = np.concatenate([np.exp(rng.uniform(np.log(1e-9), np.log(1e9), n)).astype(np.float32),   # tan^2 theta
+                        rng.integers(0, 0x7f000000, n, dtype=np.uint32).view(np.float32),       # any finite >= 0
+                        np.array([0, 0, 1e-38, 0.25, 1e-30, 1e30, 3e38, 1, np.nan], np.float32)])
+    got = _device(lib, "one_plus_sqrt", a, b)
+    want = (1.0 + np.sqrt(1.0 + a.astype(np.float64) * b.astype(np.float64))).astype(np.float32)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"{bad.size} lanes differ, e.g. a={a[bad[:4]]} b={b[bad[:4]]} got={got[bad[:4]]} want={want[bad[:4]]}"

@@ -55,6 +55,40 @@ def tree_of(m):
     return (m.name, m.parameter_values())
 
 
+def _claimed(tree, sout, sxi):
+    """Lanes where aggregatebsdf::sample (aggregatebsdf.h:122-137) hands xi to some child, recursively: x = xi0 * sum
+    is claimed by the last child k with 0 <= x - (w_0 + .. + w_{k-1}) <= w_k, all in float32 as the reference does.
+    Elsewhere (xi0 outside [0, 1], or the running residual rounding past the last weight) the reference's BsdfSample
+    keeps its uninitialised direction and flag -- indeterminate, like the sum <= eps bail-out."""
+    f = np.float32
+    if tree[0] != "Aggregate":
+        return np.ones(sout.shape[1], bool)
+    w = []
+    for k in tree[1]:
+        r = ou.ref_runtime_reflectance(k, sout)
+        w.append((r[0] + r[1]) + r[2])
+    total = f(0)
+    for wk in w:
+        total = total + wk
+    x = sxi[0].astype(f) * total
+    claimed = np.zeros(sout.shape[1], bool)
+    nxs = np.zeros(sout.shape[1], f)
+    pick = np.full(sout.shape[1], -1)
+    for i, wk in enumerate(w):
+        m = (x >= 0) & (x <= wk)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            nx = np.where(wk > np.finfo(f).eps, x / wk, f(0)).astype(f)
+        pick = np.where(m, i, pick)
+        nxs = np.where(m, nx, nxs)
+        x = (x - wk).astype(f)
+    for i, k in enumerate(tree[1]):
+        lanes = pick == i
+        if lanes.any():
+            sub = _claimed(k, sout[:, lanes], np.stack([nxs[lanes], sxi[1][lanes]]))
+            claimed[np.nonzero(lanes)[0][sub]] = True
+    return claimed
+
+
 def _batches(bbm):
     n = 1 << 20
     out = [(INP["pin"], INP["pout"])]
@@ -95,7 +129,8 @@ def test_runtime_eval_pdf_reflectance_vs_reference(bbm, key):
 def test_runtime_sample_vs_reference(bbm, key):
     """Flags identical; directions within the bar (or reproduced by the reference at xi moved by <= 2 float steps);
     the sample's pdf against the reference's runtime pdf at the GPU's direction.  Lanes where the weights sum to
-    <= eps get no sample from the reference (an indeterminate BsdfSample): there the GPU must return {0, 0, None}."""
+    <= eps, or whose xi0 no child claims (_claimed), get no sample from the reference (an indeterminate BsdfSample):
+    there the GPU must return direction 0 and flag None."""
     m = bbm.fromString(STRINGS[key])
     tree = tree_of(m)
     n = 1 << 18
@@ -108,6 +143,9 @@ def test_runtime_sample_vs_reference(bbm, key):
         wsum = ((np.float32(0) + w[0]) + w[1]) + w[2]
         live = wsum > np.finfo(np.float32).eps
         assert np.all(flag[~live] == 0) and np.all(got[:, ~live] == 0)
+        unclaimed = live & ~_claimed(tree, sout, sxi)
+        assert np.all(flag[unclaimed] == 0) and np.all(got[:3, unclaimed] == 0), f"{key}: unclaimed lanes"
+        live &= ~unclaimed
         assert np.array_equal(flag[live].astype(np.uint32), rflag[live]), f"{key}: flags"
         dok = tp._dir_ok(got[:3, live], ref[:3, live])
         bad = np.nonzero(live)[0][~dok]

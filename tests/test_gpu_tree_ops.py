@@ -211,13 +211,12 @@ def test_tree_check_f64_vs_reference(bbm, name):
     if name == "CookTorrance":
         m = bbm.CookTorrance(albedo=[0.6, 0.4, 0.3], roughness=0.3, eta=1.6)
         p = m.parameter_values()
-        ev = lambda a, b: ou.ref_eval_pdf_dd("CookTorrance", p, a, b, nthreads=8)  # noqa: E731
-        smp = lambda o, x: ou.ref_sample_double("CookTorrance", p, o, x, nthreads=8)  # noqa: E731
+        tree = ("CookTorrance", p)          # a one-leaf tree: the reference's doubleRGB bsdf_ptr on double inputs
     else:
         m = bbm.fromString(THREE)
         tree = tr.tree_of(m)
-        ev = lambda a, b: ou.ref_runtime_eval_pdf(tree, a, b, f64=True)  # noqa: E731
-        smp = lambda o, x: ou.ref_runtime_sample(tree, o, x, f64=True)  # noqa: E731
+    ev = lambda a, b: ou.ref_runtime_eval_pdf(tree, a, b, f64=True)  # noqa: E731
+    smp = lambda o, x: ou.ref_runtime_sample(tree, o, x, f64=True)  # noqa: E731
     th = (np.arange(3) * (0.5 * np.pi)) / 3
     outs = np.stack([np.sin(th), 0.0 * th, np.cos(th)])
     acc = check.run(m, check.REFLECTANCE, n, 3, torch.from_numpy(outs).cuda(), SEED, importance=True, f64=True)

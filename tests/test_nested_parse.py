@@ -105,3 +105,19 @@ def test_aggregate_children_are_copies(bbm):
     outer = bbm.Aggregate(agg, bbm.GGX())
     agg.set_parameter_values(agg.parameter_values() * 0)
     assert outer.parameter_values()[0] == np.float32(0.5)
+
+
+@pytest.mark.parametrize("s", [
+    "CookTorrance(albedo = [0.6, 0.5, 0.4], roughness = 0.25, eta = 1.6)",
+    "Aggregate(Lambertian(albedo = [0.2, 0.3, 0.4]), CookTorrance(roughness = 0.3))",
+    "Aggregate(Lambertian(albedo = [0.2, 0.3, 0.4]), CookTorrance(roughness = 0.3), GGX(roughness = 0.15))",
+    "Aggregate(Aggregate(Lambertian(albedo = [0.25, 0.25, 0.25]), Ward(roughness = [0.2, 0.3])), "
+    "Aggregate(Lambertian(albedo = [0.1, 0.2, 0.1]), GGX(roughness = 0.2)), OrenNayar)",
+])
+def test_parse_model_matches_fromstring(bbm, s):
+    """bbm_amd.parse_model (the C-ABI parser) builds the same models as the Python fromString."""
+    def flat(m):
+        if isinstance(m, bbm.AggregateModel):
+            return ("*", m.runtime, [flat(c) for c in m._children])
+        return (m.name, m.model_id, m.runtime, m.parameter_values().tolist())
+    assert flat(bbm.parse_model(s)) == flat(bbm.fromString(s))

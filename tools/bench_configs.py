@@ -216,18 +216,22 @@ def _merl_from(source):
 
 
 FIT_MATERIAL = ("bagher_sgd.fit", "alum-bronze")     # fits/bagher_sgd.fit:3, SURVEY §8(d) C5
+# the material's line of the published fit file, verbatim (data: the fitted parameter values; the GPU box has no
+# /root/reference to read it from)
+FIT_LINE = ("alum-bronze = Aggregate(Lambertian(albedo = [0.0478786, 0.0313514, 0.0200638]), Bagher(albedo = [0.0"
+            "364976, 0.664975, 0.268836], alpha = [0.014832, 0.0300126, 0.0490339], p = [0.459076, 0.450056, 0.52"
+            "9272], eta = [[6.05524, 0.235756, 0.580647], [5.05524, 0.182842, 0.476088]], K = [46.3841, 24.5961, "
+            "14.8261], Lambda = [2.60672, 2.97371, 2.7827], c = [1.12717e-07, 1.06401e-07, 5.27952e-08], k = [47."
+            "783, 36.2767, 31.6066], theta0 = [0.205635, 0.066289, -0.0661091]))")
 
 
 def fit_material():
-    """(name, model string) of the config-5 material: the reference's published Bagher fit fits/bagher_sgd.fit:3,
-    as committed in tests/golden/fits.json (the reference's fromString of every fits/ line, oracle/gen_golden.py)."""
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "fits.json")
-    with open(path) as f:
-        rows = json.load(f)[FIT_MATERIAL[0]]
-    for row in rows:
-        if row[0] == FIT_MATERIAL[1]:
-            return row[0], row[1]
-    raise KeyError(FIT_MATERIAL)
+    """(name, model) of the config-5 material: FIT_LINE ("name = model string", fits/*.fit's format) split at
+    " = " and the model built by the library's own C-ABI parser (bbm_amd.parse_model -> bbm_hip_parse_model_tree,
+    the runtime fromString an FFI caller of the fits/ files would use)."""
+    name, mstr = FIT_LINE.split(" = ", 1)
+    assert name == FIT_MATERIAL[1]
+    return name, bbm_amd.parse_model(mstr)
 
 
 def bench_fit(args, dist, rank, world):
@@ -239,10 +243,10 @@ def bench_fit(args, dist, rank, world):
     --fit-max-seconds, and the
     line reports its steps, wall time per step and the loss before / after."""
     name = "Aggregate<Lambertian,Bagher>"
-    mat, mstr = fit_material()
+    mat, material = fit_material()
     fitted = bbm_amd.BsdfModel(name)
     lin = fit.merl_linearizer()
-    reference = _merl_from(bbm_amd.fromString(mstr))
+    reference = _merl_from(material)
     loss = fit.SampledLoss(fitted, reference, "standardLog", lin, dist=dist)
     idx = fitted.parameter_indices(fit.ALL)
     probes = np.repeat(fitted.parameter_values()[None], 2 * len(idx), axis=0)
