@@ -51,7 +51,7 @@ struct Lambertian
     if (!(component & kFlagDiffuse)) return;
     if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return;
     float s, c;
-    sincosf(xi0 * float(2.0f * kPiD), &s, &c);
+    sincosf_glibc(xi0 * float(2.0f * kPiD), &s, &c);
     const float sin_t = float(safe_sqrt(1.0 - xi1));
     dir = mk3(c * sin_t, s * sin_t, safe_sqrtf(xi1));
     float rgb[3];

@@ -35,14 +35,9 @@ __host__ __device__ __forceinline__ uint64_t lin_size(const LinDesc& d)
   return (d.kind == kLinMerl) ? d.s_out[0] * d.s_out[1] * d.s_in[1] : d.s_in[0] * d.s_in[1] * d.s_out[0] * d.s_out[1];
 }
 
-// std::cos / std::sin of a float (glibc's correctly rounded cosf/sinf): rounded from double
-__device__ __forceinline__ void cossin_cr(float a, float& c, float& s)
-{
-  double sd, cd;
-  sincos(double(a), &sd, &cd);
-  c = float(cd);
-  s = float(sd);
-}
+// std::cos / std::sin of a float: glibc's cosf / sinf bit for bit (math.hpp sincosf_glibc; formerly the double
+// sincos rounded to float, which differs from glibc's 0.56-ulp results on a few lanes and costs ~3x the f64 work)
+__device__ __forceinline__ void cossin_cr(float a, float& c, float& s) { sincosf_glibc(a, &s, &c); }
 
 // spherical::convert(vec2d(phi, theta)) (core/spherical.h:58-65): (cos phi sin theta, sin phi sin theta, cos theta)
 __device__ __forceinline__ v3 sph_to_vec(float phi, float theta)
@@ -53,10 +48,10 @@ __device__ __forceinline__ v3 sph_to_vec(float phi, float theta)
   return mk3(cp * st, sp * st, ct);
 }
 
-// spherical::phi(vec3d) (core/spherical.h:42-46): atan2(y, x), + 2 pi if negative
+// spherical::phi(vec3d) (core/spherical.h:42-46): atan2(y, x) -- glibc's atan2f (math.hpp) -- + 2 pi if negative
 __device__ __forceinline__ float phi_of(v3 v)
 {
-  const float r = float(atan2(double(v.y), double(v.x)));
+  const float r = atan2f_glibc(v.y, v.x);
   return (r < 0) ? r + kPi2F : r;
 }
 

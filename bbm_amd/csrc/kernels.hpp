@@ -890,6 +890,101 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_wav
   }
 }
 
+// The pair's side of a probe evaluation: the model's parameter-independent prelude where it has one (geometry() /
+// eval_geo()), else the pair itself and the full eval.
+template<class Model, bool G = has_geo<Model>()> struct LossGeo
+{
+  typename Model::Geo g;
+  __device__ __forceinline__ void init(v3 in, v3 out) { g = Model::geometry(in, out); }
+  __device__ __forceinline__ void eval(const Model& m, uint32_t component, float* rgb) { m.eval_geo(g, component, rgb); }
+};
+template<class Model> struct LossGeo<Model, false>
+{
+  v3 in, out;
+  __device__ __forceinline__ void init(v3 i, v3 o) { in = i; out = o; }
+  __device__ __forceinline__ void eval(const Model& m, uint32_t component, float* rgb)
+  {
+    float pdf;
+    m.template eval_pdf<kModeEval>(in, out, component, rgb, pdf);
+  }
+};
+
+// Pair-major loss (the default): each thread decodes kLossPairs pairs once per call -- linearizer, reference value,
+// loss prelude, model geometry -- and runs every probe over them in a runtime loop whose model is read with uniform
+// (scalar) loads, so no probe's parameters are held in VGPRs across pairs; per probe, its kLossPairs losses are
+// summed in order (double), the wave adds them up (fixed butterfly) and lane 0 adds the wave's total into its LDS
+// row; the block's rows are summed in wave order at the end.  Against the probe-batch kernel below (k_loss): the
+// decode runs once per call instead of once per 12-probe batch, and register pressure no longer grows with the batch.
+#ifndef BBM_HIP_LOSS_PAIRS
+#define BBM_HIP_LOSS_PAIRS 2
+#endif
+#ifndef BBM_HIP_LOSS_PAIRS_WAVES
+#define BBM_HIP_LOSS_PAIRS_WAVES 1
+#endif
+constexpr int kLossPairs = BBM_HIP_LOSS_PAIRS;
+static_assert(kLossPairs >= 1, "pairs per thread of the pair-major loss kernel");
+#ifdef BBM_HIP_LOSS_PROBE_BATCH
+constexpr bool kLossPairMajor = false;       // A/B: the probe-batch kernel k_loss everywhere
+#else
+constexpr bool kLossPairMajor = true;
+#endif
+template<class Model>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BBM_HIP_LOSS_PAIRS_WAVES, 8))) void k_loss_pairs(LossArgs a)
+{
+  static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
+  extern __shared__ double part[];                       // [kBlock / 64][nprobes]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = threadIdx.x; j < (kBlock / 64) * a.nprobes; j += kBlock) part[j] = 0.0;
+  __syncthreads();
+  constexpr uint64_t span = uint64_t(kBlock) * kLossPairs;
+  for (uint64_t base = uint64_t(blockIdx.x) * span; base < a.n; base += uint64_t(gridDim.x) * span)
+  {
+    LossGeo<Model> geo[kLossPairs];
+    LossSample smp[kLossPairs];
+    bool live[kLossPairs];
+#pragma unroll
+    for (int k = 0; k < kLossPairs; ++k)
+    {
+      const uint64_t i = base + uint64_t(k) * kBlock + threadIdx.x;
+      live[k] = i < a.n;
+      if (!live[k]) continue;
+      v3 in, out;
+      if (a.pairs[0] != nullptr)
+      {
+        in = mk3(a.pairs[0][i], a.pairs[1][i], a.pairs[2][i]);
+        out = mk3(a.pairs[3][i], a.pairs[4][i], a.pairs[5][i]);
+      }
+      else lin_pair(a.lin, a.begin + i, in, out);
+      const float ref[3] = {a.ref_r[i], a.ref_g[i], a.ref_b[i]};
+      smp[k] = loss_prepare(a.loss_kind, in, out, ref);
+      geo[k].init(in, out);
+    }
+    for (int j = 0; j < a.nprobes; ++j)
+    {
+      const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(j) * kLossModelBytes);
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kLossPairs; ++k)
+      {
+        if (!live[k]) continue;
+        float rgb[3];
+        geo[k].eval(m, a.component, rgb);
+        acc += double(sample_loss(a.loss_kind, smp[k], rgb));
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) part[wave * a.nprobes + j] += acc;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < a.nprobes; j += kBlock)
+  {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w * a.nprobes + j];
+    a.block_sums[size_t(blockIdx.x) * a.nprobes + j] = t;
+  }
+}
+
 // sums[p] = sum over blocks of block_sums[b][p], in block order (one workgroup per probe; fixed tree)
 __global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums, int nblocks, int nprobes, double* sums);
 
@@ -898,11 +993,23 @@ int launch_loss(const LossArgs& a0, hipStream_t s)
 {
   if (const int rc = host_prepare<Model>::run(s)) return rc;
   LossArgs a = a0;
-  uint64_t blocks = (a.n + kBlock - 1) / kBlock;
-  if (blocks < 1) blocks = 1;
-  if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
   hipLaunchKernelGGL((k_loss_models<Model>), dim3(unsigned((a.nprobes + 63) / 64)), dim3(64), 0, s, a);
-  hipLaunchKernelGGL((k_loss<Model>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  uint64_t blocks;
+  const size_t lds = size_t(kBlock / 64) * size_t(a.nprobes) * sizeof(double);
+  if (kLossPairMajor && lds <= 48 * 1024)       // up to 1536 probes; more take the probe-batch kernel
+  {
+    blocks = (a.n + uint64_t(kBlock) * kLossPairs - 1) / (uint64_t(kBlock) * kLossPairs);
+    if (blocks < 1) blocks = 1;
+    if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
+    hipLaunchKernelGGL((k_loss_pairs<Model>), dim3(unsigned(blocks)), dim3(kBlock), lds, s, a);
+  }
+  else
+  {
+    blocks = (a.n + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
+    hipLaunchKernelGGL((k_loss<Model>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  }
   hipLaunchKernelGGL(k_loss_final, dim3(unsigned(a.nprobes)), dim3(kBlock), 0, s, a.block_sums, int(blocks), a.nprobes,
                      a.sums);
   const hipError_t e = hipGetLastError();

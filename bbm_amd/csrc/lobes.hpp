@@ -112,7 +112,7 @@ struct Ward
     dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
     if (!((component & kFlagSpecular) && xi_valid(xi0, xi1))) return;
     float s, c;
-    sincosf(kPi2F * xi0, &s, &c);
+    sincosf_glibc(kPi2F * xi0, &s, &c);
     const float cx = c * rx, cy = s * ry;
     const float r = div_nr(1.0f, sqrtf(sqnorm2(cx, cy)));
     const float csx = cx * r, csy = cy * r;
@@ -162,7 +162,7 @@ struct PhongLobe
     dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
     if (!((component & kFlagSpecular) && xi_valid(xi0, xi1))) return;
     float sp, cp;
-    sincosf(xi0 * kPi2F, &sp, &cp);
+    sincosf_glibc(xi0 * kPi2F, &sp, &cp);
     const float cosT = float(pow(double(xi1), 1.0 / (s + 1)));
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
     dir = to_global(mk3(-out.x, -out.y, out.z), mk3(cp * sinT, sp * sinT, cosT));
@@ -240,7 +240,7 @@ struct Lafortune
     dir = mk3(0.0f, 0.0f, 0.0f); pdf = 0.0f; flag = kFlagNone;
     if (!((component & kFlagSpecular) && xi_valid(xi0, xi1))) return;
     float sp, cp;
-    sincosf(xi0 * kPi2F, &sp, &cp);
+    sincosf_glibc(xi0 * kPi2F, &sp, &cp);
     const float cosT = float(pow(double(xi1), 1.0 / (s + 1)));
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
     dir = to_global(mk3(cx * out.x, cy * out.y, cz * out.z), mk3(cp * sinT, sp * sinT, cosT));
@@ -401,12 +401,12 @@ struct AshikhminShirley
     {
       float phi = float(atan(sqrt((su + 1.0) / (sv + 1.0)) * double(tanf(xi0 * kPi2F))));
       phi = ((xi0 > 0.25) && (xi0 < 0.75)) ? phi + kPiF : phi;
-      sincosf(phi, &sp, &cp);
+      sincosf_glibc(phi, &sp, &cp);
       cosT = float(pow(double(xi1), 1.0 / ((su * (cp * cp)) + (sv * (sp * sp)) + 1.0)));
     }
     else
     {
-      sincosf(xi0 * kPi2F, &sp, &cp);
+      sincosf_glibc(xi0 * kPi2F, &sp, &cp);
       cosT = float(pow(double(xi1), 1.0 / (su + 1.0)));
     }
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
@@ -536,11 +536,11 @@ struct LowSmooth
     const float ro = sqrtf(ro2);
     const double rp = double(ri + ro), rm = double(ri - ro);
     const float scale = float(sqrt((1.0 + B * (rp * rp)) / (1.0 + B * (rm * rm))));
-    float phio = atan2f(out.y, out.x);
+    float phio = atan2f_glibc(out.y, out.x);
     phio = (phio < 0) ? phio + kPi2F : phio;
     const float phi = float(2.0 * double(atanf(tanf(xi1 * kPiF) * scale)) + phio);
     float sp, cp;
-    sincosf(phi, &sp, &cp);
+    sincosf_glibc(phi, &sp, &cp);
     dir = mk3(cp * ri, sp * ri, float(safe_sqrt(1.0 - ri * ri)));
     float rgb[3];
     eval_pdf<kModePdf>(dir, out, component, rgb, pdf);

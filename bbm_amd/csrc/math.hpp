@@ -512,6 +512,106 @@ __device__ __forceinline__ float erff_glibc(float x)
   return (x != x) ? x : res;
 }
 
+// glibc 2.35's atan2f (sysdeps/ieee754/flt-32/e_atan2f.c with s_atanf.c: Sun fdlibm's float algorithms, no FMA
+// variant) -- what the reference's spherical::phi (core/spherical.h:42-46) and every float atan2 call -- restated op
+// for op in float arithmetic: q = |y / x| (IEEE division), atan(q) by fdlibm's reduction to one of four breakpoints
+// (atan 0.5, 1, 1.5, inf as hi + lo; one more IEEE division) and its 11-term odd polynomial, then the quadrant
+// fix-ups with pi_lo.  Not correctly rounded, hence restated rather than rounded from a double atan2.  Same float as
+// this machine's libm on 6e7 random pairs (unit-vector components, any finite floats, mixed magnitudes) and on every
+// combination of zeros, infinities and NaN (oracle/atan2f_glibc_check.c); branch-free but for the two divisions.
+namespace fdlibm_atan {
+constexpr float kHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+constexpr float kLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+constexpr float kT[11] = {3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                          9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                          4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f};
+// atanf (s_atanf.c) of a float x >= 0 below 2^25
+__device__ __forceinline__ float atan_pos(float x)
+{
+  const uint32_t ix = __float_as_uint(x);
+  const int id = (ix < 0x3f300000u) ? 0 : ((ix < 0x3f980000u) ? 1 : ((ix < 0x401c0000u) ? 2 : 3));
+  const float num = (id == 0) ? 2.0f * x - 1.0f : ((id == 1) ? x - 1.0f : ((id == 2) ? x - 1.5f : -1.0f));
+  const float den = (id == 0) ? 2.0f + x : ((id == 1) ? x + 1.0f : ((id == 2) ? 1.0f + 1.5f * x : x));
+  const bool small = ix < 0x3ee00000u;                           // |x| < 0.4375: no reduction
+  const float t = small ? x : __fdiv_rn(num, den);
+  const float z = t * t;
+  const float w = z * z;
+  const float s1 = z * (kT[0] + w * (kT[2] + w * (kT[4] + w * (kT[6] + w * (kT[8] + w * kT[10])))));
+  const float s2 = w * (kT[1] + w * (kT[3] + w * (kT[5] + w * (kT[7] + w * kT[9]))));
+  const float hi = (id == 0) ? kHi[0] : ((id == 1) ? kHi[1] : ((id == 2) ? kHi[2] : kHi[3]));
+  const float lo = (id == 0) ? kLo[0] : ((id == 1) ? kLo[1] : ((id == 2) ? kLo[2] : kLo[3]));
+  return small ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+}
+}  // namespace fdlibm_atan
+
+__device__ __forceinline__ float atan2f_glibc(float y, float x)
+{
+  using namespace fdlibm_atan;
+  constexpr float pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+                  pi_lo = -8.7422776573e-08f;
+  const uint32_t hx = __float_as_uint(x), hy = __float_as_uint(y), ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
+  const bool yneg = (hy >> 31) != 0, xneg = (hx >> 31) != 0;
+  const int m = int(yneg) | (int(xneg) << 1);
+  const float big = kHi[3] + kLo[3];
+  // the general case (finite, nonzero x != 1 and y): atan |y / x|, then the quadrant
+  const int k = (int(iy) - int(ix)) >> 23;
+  const float q = __builtin_fabsf(__fdiv_rn(y, x));
+  float z = (__float_as_uint(q) >= 0x4c000000u) ? big : atan_pos(q);
+  z = (k > 60) ? pi_o_2 + 0.5f * pi_lo : ((xneg && k < -60) ? 0.0f : z);
+  float r = (m == 0) ? z : ((m == 1) ? -z : ((m == 2) ? pi - (z - pi_lo) : (z - pi_lo) - pi));
+  // x = 1: atanf(y) itself
+  const float a1 = (iy >= 0x4c000000u) ? big : atan_pos(__builtin_fabsf(y));
+  r = (hx == 0x3f800000u) ? (yneg ? -a1 : a1) : r;
+  // infinities and zeros
+  r = (iy == 0x7f800000u) ? (yneg ? -pi_o_2 : pi_o_2) : r;
+  const float xinf = (iy == 0x7f800000u) ? ((m == 0) ? pi_o_4 : (m == 1) ? -pi_o_4 : (m == 2) ? 3.0f * pi_o_4 : -3.0f * pi_o_4)
+                                         : ((m == 0) ? 0.0f : (m == 1) ? -0.0f : (m == 2) ? pi : -pi);
+  r = (ix == 0x7f800000u && hx != 0x3f800000u) ? xinf : r;
+  r = (ix == 0) ? (yneg ? -pi_o_2 : pi_o_2) : r;
+  r = (iy == 0) ? ((m < 2) ? y : ((m == 2) ? pi : -pi)) : r;
+  return (ix > 0x7f800000u || iy > 0x7f800000u) ? x + y : r;
+}
+
+// glibc 2.35's sinf and cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h, sincosf_data.c -- the Arm
+// optimized-routines algorithms behind the reference's bbm::cossin(float) = (std::cos, std::sin), backbone/native/
+// include/backbone/math.h:126, on every sampler's angle), restated in IEEE double ops as the FMA-contracted ifunc
+// variant, both from one shared reduction.  |y| below 0.75 (pi/4's abstop12): the polynomials in y directly (y itself
+// / 1 below 2^-12); |y| < 120: the quadrant n from y (2/pi) 2^24 truncated (+2^23, >> 24), r = y - n pi/2 by one
+// FMA, sin(r) by the odd and cos(r) by the even polynomial, swapped in odd quadrants and signed per quadrant.  The
+// coefficients are glibc's table (__sincosf_table[0]; table [1] is its even half negated, which the sign select
+// reproduces exactly).  Every float |y| < 120 gives glibc's sinf and cosf bit for bit (oracle/sincosf_glibc_check.c,
+// all 2.2e9).  Larger |y|, inf and NaN (no sampler angle) take the device library's sincosf.
+__device__ __forceinline__ void sincosf_glibc(float y, float* sp, float* cp)
+{
+  constexpr double kC0 = 1.0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5, kC3 = -0x1.6c087e89a359dp-10,
+                   kC4 = 0x1.99343027bf8c3p-16;
+  constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = -0x1.994eb3774cf24p-13;
+  const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ffu;
+  if (__builtin_expect(top >= 0x42fu, false))
+  {
+    sincosf(y, sp, cp);
+    return;
+  }
+  double x = double(y);
+  int n = 0;
+  if (top >= 0x3f4u)
+  {
+    n = (int32_t(x * 0x1.45f306dc9c883p+23) + 0x800000) >> 24;
+    x = __builtin_fma(-double(n), 0x1.921fb54442d18p+0, x);
+  }
+  const double x2 = x * x;
+  const double xs = ((n ^ (n >> 1)) & 1) ? -x : x;               // sign[n & 3] = {1, -1, -1, 1}
+  const double x3 = xs * x2;
+  const double s = __builtin_fma(__builtin_fma(x2, kS3, kS2), x3 * x2, __builtin_fma(x3, kS1, xs));
+  const double x4 = x2 * x2;
+  double c = __builtin_fma(x4 * x2, __builtin_fma(x2, kC4, kC3), __builtin_fma(x4, kC2, __builtin_fma(x2, kC1, kC0)));
+  c = (n & 2) ? -c : c;                                          // __sincosf_table[1]
+  const bool tiny = top < 0x398u;
+  const float so = tiny ? y : float(s), co = tiny ? 1.0f : float(c);
+  *sp = (n & 1) ? co : so;
+  *cp = (n & 1) ? so : co;
+}
+
 // a / m for a normal float a >= 0 and a small integer m (a loop counter) with its reciprocal rm = RN(1/m) known:
 // q = a rm corrected once by the exact remainder -- the correctly rounded quotient (as div_nr) without v_rcp_f32
 __device__ __forceinline__ float div_small(float a, float m, float rm)

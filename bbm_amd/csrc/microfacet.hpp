@@ -138,7 +138,7 @@ struct GGX
     const float r = sqrtf(xi0);
     const float phi = float(((xi1 < a) ? double(div_nr(xi1, a)) : 1.0 + ddiv_nr(double(xi1 - a), 1.0 - a)) * kPiF);
     float sp, cp;
-    sincosf(phi, &sp, &cp);
+    sincosf_glibc(phi, &sp, &cp);
     const float P1 = r * cp;
     const float P2 = float(((xi1 < a) ? 1.0 : double(vs.z)) * r * sp);
     const float sq = float(safe_sqrt(1.0 - P1 * P1 - P2 * P2));
@@ -185,7 +185,7 @@ struct PhongNdf
     const float cosT = float(pow(double(xi0), 1.0 / (sharpness + 2)));
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
     float sp, cp;
-    sincosf(xi1 * float(2.0f * kPiD), &sp, &cp);
+    sincosf_glibc(xi1 * float(2.0f * kPiD), &sp, &cp);
     return mk3(cp * sinT, sp * sinT, cosT);
   }
 };
@@ -298,7 +298,7 @@ struct StudentT
   {
     if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
     float sp, cp;
-    sincosf(float(2.0f * kPiD) * xi0, &sp, &cp);
+    sincosf_glibc(float(2.0f * kPiD) * xi0, &sp, &cp);
     float normalization;
     if (Aniso)
     {
@@ -411,7 +411,7 @@ struct LowNdf
     const float cosT = float((1.0 + B - term) / B);
     const float sinT = float(safe_sqrt(1.0 - cosT * cosT));
     float sp, cp;
-    sincosf(xi1 * float(2.0f * kPiD), &sp, &cp);
+    sincosf_glibc(xi1 * float(2.0f * kPiD), &sp, &cp);
     return mk3(cp * sinT, sp * sinT, cosT);
   }
 

@@ -69,8 +69,14 @@ struct Bagher
     // glibc's powf and expf restated bit for bit (math.hpp; the correctly rounded power differs from glibc's on ~0.1 %
     // of the lanes, and each such lane moved G by up to 1e-2 relative).  th - theta0 may be <= 0 on lanes the select
     // below discards.
-    const float g = 1.0f + Lambda[j] * (1.0f - expf_glibc(c[j] * powf_glibc(th - theta0[j], k[j])));
-    return (th > theta0[j]) ? g : 1.0f;
+    return (th > theta0[j]) ? g1_tail(th - theta0[j], c[j], k[j], Lambda[j]) : 1.0f;
+  }
+  // 1 + Lambda (1 - exp(c d^k)) out of line: the exact powf / expf hold ~40 VGPRs of f64 temporaries, and inlined
+  // into each of the six (channel, direction) branches they set the register budget of every kernel around them
+  // (the loss kernel spilled 124 VGPRs instead of 69) although at the default theta0 = pi/2 no lane takes them
+  __device__ __attribute__((noinline)) static float g1_tail(float d, float c, float k, float Lambda)
+  {
+    return 1.0f + Lambda * (1.0f - expf_glibc(c * powf_glibc(d, k)));
   }
   // the same for an upper-hemisphere direction with squared chord q: lanes below the conservative threshold have
   // theta <= theta0 and G1 = 1; the others evaluate G1 exactly as above, on a branch (the shadowing term's double

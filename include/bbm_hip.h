@@ -459,8 +459,8 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
 /* ---------------------------------------------------------------- device math verification */
 
 /* The device restatements of the host libm float functions the reference's native backbone calls (glibc 2.35's
- * expf, logf, powf, erff, erfcf: bbm_amd/csrc/math.hpp), evaluated elementwise on n device floats:
- * out[i] = f(a[i]) (f(a[i], b[i]) for powf and ONE_PLUS_SQRT; b may be NULL otherwise).  For pinning them against the host libm on
+ * expf, logf, powf, erff, erfcf, sinf, cosf, atan2f: bbm_amd/csrc/math.hpp), evaluated elementwise on n device floats:
+ * out[i] = f(a[i]) (f(a[i], b[i]) for powf, ONE_PLUS_SQRT, atan2f; b may be NULL otherwise).  For pinning them against the host libm on
  * the machine that runs the reference (tests/test_gpu_libm.py); not on any BSDF path. */
 #define BBM_HIP_LIBM_EXPF 0
 #define BBM_HIP_LIBM_LOGF 1
@@ -468,6 +468,9 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
 #define BBM_HIP_LIBM_ERFF 3
 #define BBM_HIP_LIBM_ERFCF 4
 #define BBM_HIP_LIBM_ONE_PLUS_SQRT 5   /* float(1.0 + sqrt(1.0 + (double)a * b)), the GGX G1 denominator */
+#define BBM_HIP_LIBM_SINF 6
+#define BBM_HIP_LIBM_COSF 7
+#define BBM_HIP_LIBM_ATAN2F 8       /* atan2f(a, b) */
 int bbm_hip_libm_eval(int func, const float* a, const float* b, float* out, size_t n, void* stream);
 
 #ifdef __cplusplus

@@ -431,6 +431,9 @@ int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n)
       case 2: out[i] = powf(a[i], b[i]); break;
       case 3: out[i] = erff(a[i]); break;
       case 4: out[i] = erfcf(a[i]); break;
+      case 6: out[i] = sinf(a[i]); break;
+      case 7: out[i] = cosf(a[i]); break;
+      case 8: out[i] = atan2f(a[i], b[i]); break;
       default: return -1;
     }
   }

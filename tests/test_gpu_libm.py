@@ -13,7 +13,7 @@ from tests import oracle_util as ou
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4, "one_plus_sqrt": 5}
+FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4, "one_plus_sqrt": 5, "sinf": 6, "cosf": 7, "atan2f": 8}
 
 
 @pytest.fixture(scope="module")
@@ -99,3 +99,36 @@ def test_one_plus_sqrt_bitexact(lib):
     want = (1.0 + np.sqrt(1.0 + a.astype(np.float64) * b.astype(np.float64))).astype(np.float32)
     bad = np.nonzero(~_same(got, want))[0]
     assert bad.size == 0, f"{bad.size} lanes differ, e.g. a={a[bad[:4]]} b={b[bad[:4]]} got={got[bad[:4]]} want={want[bad[:4]]}"
+
+
+@pytest.mark.parametrize("func", ["sinf", "cosf"])
+def test_sincos_bitexact_sweep(lib, func):
+    """sincosf_glibc on its exact domain |x| < 120 (every sampler angle): a strided sweep of both signs against the
+    host's sinf / cosf; beyond it (and inf / NaN) the device library's sincosf: finite where the host's is, NaN where
+    it is NaN."""
+    u = np.arange(3, 0x42f00000, 97, dtype=np.uint32)
+    a = np.concatenate([u, u | np.uint32(0x80000000)]).view(np.float32)
+    got, want = _device(lib, func, a), _host(func, a)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"{func}: {bad.size} lanes differ, e.g. x={a[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"
+    big = np.array([120, -120, 1e4, 3e38, np.inf, -np.inf, np.nan], np.float32)
+    gb, wb = _device(lib, func, big), _host(func, big)
+    assert np.array_equal(np.isnan(gb), np.isnan(wb)) and np.allclose(gb[~np.isnan(wb)], wb[~np.isnan(wb)], atol=1e-6)
+
+
+def test_atan2f_bitexact(lib):
+    """atan2f_glibc (fdlibm's e_atan2f.c / s_atanf.c, the reference's spherical::phi) against the host's atan2f:
+    unit-vector components, any finite floats, mixed magnitudes, and the zero / infinity / NaN combinations."""
+    rng = np.random.default_rng(20261019)
+    n = 1 << 22
+    v = rng.normal(size=(3, n))
+    v /= np.linalg.norm(v, axis=0)
+    sp = np.array([0, -0.0, 1, -1, np.inf, -np.inf, np.nan, 1e-45, 3e38, 0.5], np.float32)
+    ys = [v[1].astype(np.float32), rng.integers(0, 0xff800000, n, dtype=np.uint32).view(np.float32),
+          (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-40, 40, n)).astype(np.float32), np.repeat(sp, sp.size)]
+    xs = [v[0].astype(np.float32), rng.integers(0, 0xff800000, n, dtype=np.uint32).view(np.float32),
+          (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-40, 40, n)).astype(np.float32), np.tile(sp, sp.size)]
+    a, b = np.concatenate(ys), np.concatenate(xs)
+    got, want = _device(lib, "atan2f", a, b), _host("atan2f", a, b)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"{bad.size} lanes differ, e.g. y={a[bad[:4]]} x={b[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"

@@ -183,3 +183,19 @@ def test_erff_erfcf_restatements_match_host_libm():
     mismatches)."""
     out = _run_check("erfcf_glibc_check", 31)
     assert "erfcf 0 mismatches, erff 0 mismatches" in out, out
+
+
+def test_sinf_cosf_restatements_match_host_libm():
+    """math.hpp sincosf_glibc restates glibc's sinf / cosf (the reference's bbm::cossin of a float, on every sampler
+    angle); oracle/sincosf_glibc_check runs the same double steps in C against this host's libm on every 7th float
+    with |x| < 120 here (stride 1: all 2.2e9, 0 mismatches)."""
+    out = _run_check("sincosf_glibc_check", 7)
+    assert "cosf mismatches 0, sinf mismatches 0" in out, out
+
+
+def test_atan2f_restatement_matches_host_libm():
+    """math.hpp atan2f_glibc restates glibc's atan2f (fdlibm's float e_atan2f.c / s_atanf.c; the reference's
+    spherical::phi); oracle/atan2f_glibc_check runs the same float steps in C against this host's libm on 3 x 2e6
+    random pairs here (3 x 2e7 in DESIGN.md) and every zero / infinity / NaN combination."""
+    out = _run_check("atan2f_glibc_check", 2000000)
+    assert "0 mismatches" in out, out
