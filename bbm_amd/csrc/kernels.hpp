@@ -919,7 +919,7 @@ template<class Model> struct LossGeo<Model, false>
 #define BBM_HIP_LOSS_PAIRS 2
 #endif
 #ifndef BBM_HIP_LOSS_PAIRS_WAVES
-#define BBM_HIP_LOSS_PAIRS_WAVES 1
+#define BBM_HIP_LOSS_PAIRS_WAVES 3
 #endif
 constexpr int kLossPairs = BBM_HIP_LOSS_PAIRS;
 static_assert(kLossPairs >= 1, "pairs per thread of the pair-major loss kernel");
@@ -928,8 +928,12 @@ constexpr bool kLossPairMajor = false;       // A/B: the probe-batch kernel k_lo
 #else
 constexpr bool kLossPairMajor = true;
 #endif
+// minimum waves per SIMD of k_loss_pairs; measured on config 5 (profiles/r04_ab_fit_loss_kernel.txt): 2 pairs per
+// thread at 3 waves 0.607-0.610 ms per compass step, 1 pair at 3 waves 0.626-0.632, unconstrained (2 waves, 218
+// VGPRs) 0.79-0.81, the probe-batch kernel 0.654-0.656.  The He family keeps the compiler's choice (models.hpp).
+template<class Model> struct loss_pair_waves { static constexpr int value = BBM_HIP_LOSS_PAIRS_WAVES; };
 template<class Model>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BBM_HIP_LOSS_PAIRS_WAVES, 8))) void k_loss_pairs(LossArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pair_waves<Model>::value, 8))) void k_loss_pairs(LossArgs a)
 {
   static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
   extern __shared__ double part[];                       // [kBlock / 64][nprobes]

@@ -518,7 +518,8 @@ __device__ __forceinline__ float erff_glibc(float x)
 // (atan 0.5, 1, 1.5, inf as hi + lo; one more IEEE division) and its 11-term odd polynomial, then the quadrant
 // fix-ups with pi_lo.  Not correctly rounded, hence restated rather than rounded from a double atan2.  Same float as
 // this machine's libm on 6e7 random pairs (unit-vector components, any finite floats, mixed magnitudes) and on every
-// combination of zeros, infinities and NaN (oracle/atan2f_glibc_check.c); branch-free but for the two divisions.
+// combination of zeros, infinities and NaN, and at x = 1 (glibc's atanf shortcut, the same float) for every 13th y
+// (oracle/atan2f_glibc_check.c).  Branch-free: selects around two IEEE divisions.
 namespace fdlibm_atan {
 constexpr float kHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
 constexpr float kLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
@@ -559,14 +560,12 @@ __device__ __forceinline__ float atan2f_glibc(float y, float x)
   float z = (__float_as_uint(q) >= 0x4c000000u) ? big : atan_pos(q);
   z = (k > 60) ? pi_o_2 + 0.5f * pi_lo : ((xneg && k < -60) ? 0.0f : z);
   float r = (m == 0) ? z : ((m == 1) ? -z : ((m == 2) ? pi - (z - pi_lo) : (z - pi_lo) - pi));
-  // x = 1: atanf(y) itself
-  const float a1 = (iy >= 0x4c000000u) ? big : atan_pos(__builtin_fabsf(y));
-  r = (hx == 0x3f800000u) ? (yneg ? -a1 : a1) : r;
+  // (glibc's x = 1 shortcut, atanf(y), is this same float: y / 1 = y, |y| >= 2^25 -> hi + lo = pi_o_2 + pi_lo / 2)
   // infinities and zeros
   r = (iy == 0x7f800000u) ? (yneg ? -pi_o_2 : pi_o_2) : r;
   const float xinf = (iy == 0x7f800000u) ? ((m == 0) ? pi_o_4 : (m == 1) ? -pi_o_4 : (m == 2) ? 3.0f * pi_o_4 : -3.0f * pi_o_4)
                                          : ((m == 0) ? 0.0f : (m == 1) ? -0.0f : (m == 2) ? pi : -pi);
-  r = (ix == 0x7f800000u && hx != 0x3f800000u) ? xinf : r;
+  r = (ix == 0x7f800000u) ? xinf : r;
   r = (ix == 0) ? (yneg ? -pi_o_2 : pi_o_2) : r;
   r = (iy == 0) ? ((m < 2) ? y : ((m == 2) ? pi : -pi)) : r;
   return (ix > 0x7f800000u || iy > 0x7f800000u) ? x + y : r;

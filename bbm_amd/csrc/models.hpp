@@ -24,6 +24,9 @@ template<class B> struct loss_waves<Aggregate<Lambertian, B>> { static constexpr
 template<class B> struct eval_grid_cap<Aggregate<Lambertian, B>> { static constexpr uint64_t value = eval_grid_cap<B>::value; };
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
+template<class B> struct loss_pair_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_pair_waves<B>::value; };
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct loss_pair_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
 // Bagher's evaluation holds ~180 VGPRs (two waves per SIMD) unconstrained.  Measured (10M pairs, eval+pdf,
 // tools/gpu_ab_he.sh): Bagher 0.238 / 0.203 / 0.262 ms and Aggregate(Lambertian, Bagher) 0.266 / 0.231 / 0.324 ms
 // at 2 / 3 / 4 waves per SIMD -- three it is.

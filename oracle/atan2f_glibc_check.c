@@ -4,7 +4,8 @@
  * atan2 of two floats -> backbone/native/include/backbone/math.h:87-88 std::atan2 -> atan2f).
  *
  *   atan2f_glibc_check [n]   n random (y, x) pairs per input class (default 2e8): unit-vector components (the
- *                            callers' domain), any finite floats, mixed magnitudes; plus zeros, infinities, NaN
+ *                            callers' domain), any finite floats, mixed magnitudes; plus zeros, infinities, NaN,
+ *                            and x = 1 against every 13th y
  *
  * atan(y / x) by fdlibm's float atanf: four breakpoints (atan 0.5, 1, 1.5, inf as hi + lo), an 11-term odd
  * polynomial split in two Horner chains, all in float arithmetic; the quadrant fix-ups with pi_lo.  The constants are
@@ -54,12 +55,8 @@ static float atan2f_r(float y, float x)
   const uint32_t hx = bits(x), hy = bits(y), ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
   if (ix > 0x7f800000u || iy > 0x7f800000u) return x + y;
   const int m = (int)(((hy >> 31) & 1u) | ((hx >> 30) & 2u));
-  if (hx == 0x3f800000u)                                          /* x = 1: atanf(y) */
-  {
-    if (iy >= 0x4c000000u) return (hy >> 31) ? -atanhi[3] - atanlo[3] : atanhi[3] + atanlo[3];
-    const float a = atanf_pos(fabsf(y));
-    return (hy >> 31) ? -a : a;
-  }
+  /* glibc's x = 1 shortcut (atanf(y)) is not restated: the general path below gives the same float there
+     (y / 1 = y; |y| >= 2^25: hi + lo = pi_o_2 + pi_lo / 2), which the x = 1 sweep in main checks */
   if (iy == 0) return (m < 2) ? y : ((m == 2) ? pi : -pi);
   if (ix == 0) return (hy >> 31) ? -pi_o_2 : pi_o_2;
   if (ix == 0x7f800000u)
@@ -101,6 +98,14 @@ int main(int argc, char** argv)
       const float got = atan2f_r(sp[i], sp[j]), want = atan2f(sp[i], sp[j]);
       if (bits(got) != bits(want) && !(isnan(got) && isnan(want)) && bad++ < 8)
         printf("atan2f(%a, %a): restated %a, libm %a\n", sp[i], sp[j], got, want);
+      ++tested;
+    }
+  for (uint32_t u = 0; u < 0x7f800000u; u += 13)                  /* x = 1, every 13th y of both signs */
+    for (int sgn = 0; sgn < 2; ++sgn)
+    {
+      const float y = fromb(u | (sgn ? 0x80000000u : 0u));
+      const float got = atan2f_r(y, 1.0f), want = atan2f(y, 1.0f);
+      if (bits(got) != bits(want) && bad++ < 8) printf("atan2f(%a, 1): restated %a, libm %a\n", y, got, want);
       ++tested;
     }
   for (int cls = 0; cls < 3; ++cls)

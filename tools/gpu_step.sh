@@ -66,7 +66,7 @@ step_pmc() {
     local sel=(--models "$M")
     case $w in
       evalpdf) sel=(--model "$M" --pairs "$units" --no-exact --graph off);;
-      fit) sel=();;
+      fit) sel=(--fit-max-steps 0);;
       models) sel=(--models "$M" --graph off);;
     esac
     for P in "$SQ8" "$LANE"; do
