@@ -68,12 +68,14 @@ struct Aggregate
     return (sum > kEpsF) ? (runtime ? tm : div_nr(ip, sum)) : 0.0f;
   }
 
-  template<int MODE>
+  // exact mode (bbm_hip_set_exact_subnormals) for whichever child has one
+  static constexpr bool kHasExact = model_has_exact<A>() || model_has_exact<B>();
+  template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     float ra[3], rb[3], pa, pb;
-    a.template eval_pdf<MODE>(in, out, component, ra, pa);
-    b.template eval_pdf<MODE>(in, out, component, rb, pb);
+    model_eval_pdf<MODE, EXACT>(a, in, out, component, ra, pa);
+    model_eval_pdf<MODE, EXACT>(b, in, out, component, rb, pb);
     rgb[0] = ra[0] + rb[0];
     rgb[1] = ra[1] + rb[1];
     rgb[2] = ra[2] + rb[2];

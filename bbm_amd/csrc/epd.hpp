@@ -219,8 +219,18 @@ struct VanGinneken
   template<class NDF>
   __device__ __forceinline__ static float eval(const NDF& ndf, v3 in, v3 out, v3 m, float inm, float outm)
   {
-    // spherical::phi of both directions: glibc's atan2f restated (math.hpp atan2f_glibc), the reference's float
+#ifdef BBM_HIP_EPD_PHI_GLIBC
+    // spherical::phi of both directions as the reference's own floats (glibc's atan2f restated, math.hpp): measured
+    // 0.234 -> 0.341 ms per 10 M pairs (profiles/r04_ab_models.txt) for bit-identical lanes 0.8345 -> 0.8358 --
+    // the G1 table's index map and the NDF's exponentials leave the rest -- so not the default
     const float phi = fabsf(phi_of(in) - phi_of(out));
+#else
+    // spherical::phi is glibc's atan2f (not correctly rounded); here the device library's f32 atan2 instead: phi only
+    // scales lambda (continuously), each phi within ~2 ulp, so G1 moves by <= ~2e-6 relative where the two azimuths
+    // nearly cancel and far less elsewhere
+    auto phif = [](v3 v) { const float r = atan2f(v.y, v.x); return (r < 0) ? r + kPi2F : r; };
+    const float phi = fabsf(phif(in) - phif(out));
+#endif
     const float lambda = float(4.41 * double(phi) / (4.41 * double(phi) + 1.0));
     const float gi = ndf.G1(in, m), go = ndf.G1(out, m);
     const float gio = gi * go;

@@ -69,19 +69,8 @@ struct EvalArgs
   ParamBlock p;
 };
 
-// Models with an exact-subnormal evaluation (Microfacet over Beckmann: Model::kHasExact, microfacet.hpp) get a
-// second instantiation of the eval kernels, launched when bbm_hip_set_exact_subnormals is on.
-template<class Model> constexpr bool model_has_exact()
-{
-  if constexpr (requires { Model::kHasExact; }) return Model::kHasExact;
-  else return false;
-}
-template<int MODE, bool EXACT, class Model>
-__device__ __forceinline__ void model_eval_pdf(const Model& m, v3 in, v3 out, uint32_t comp, float* rgb, float& pdf)
-{
-  if constexpr (EXACT) m.template eval_pdf<MODE, true>(in, out, comp, rgb, pdf);
-  else m.template eval_pdf<MODE>(in, out, comp, rgb, pdf);
-}
+// exact mode (model_has_exact / model_eval_pdf: math.hpp)
+
 // process-wide switch (bbm_hip_set_exact_subnormals; initial value from BBM_HIP_EXACT_SUBNORMALS)
 inline std::atomic<int>& exact_subnormals()
 {
@@ -921,7 +910,11 @@ template<class Model> struct LossGeo<Model, false>
 #ifndef BBM_HIP_LOSS_PAIRS_WAVES
 #define BBM_HIP_LOSS_PAIRS_WAVES 3
 #endif
+#ifndef BBM_HIP_LOSS_PROBE_UNROLL
+#define BBM_HIP_LOSS_PROBE_UNROLL 1
+#endif
 constexpr int kLossPairs = BBM_HIP_LOSS_PAIRS;
+constexpr int kLossProbeUnroll = BBM_HIP_LOSS_PROBE_UNROLL;   // probes evaluated per iteration of the probe loop
 static_assert(kLossPairs >= 1, "pairs per thread of the pair-major loss kernel");
 #ifdef BBM_HIP_LOSS_PROBE_BATCH
 constexpr bool kLossPairMajor = false;       // A/B: the probe-batch kernel k_loss everywhere
@@ -940,8 +933,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int j = threadIdx.x; j < (kBlock / 64) * a.nprobes; j += kBlock) part[j] = 0.0;
   __syncthreads();
+  // this workgroup's contiguous share of the samples: equal to one sample per thread and pass across the grid, so
+  // no workgroup runs an extra pass the others do not (the grid is a multiple of the resident workgroups)
   constexpr uint64_t span = uint64_t(kBlock) * kLossPairs;
-  for (uint64_t base = uint64_t(blockIdx.x) * span; base < a.n; base += uint64_t(gridDim.x) * span)
+  const uint64_t lo = a.n * blockIdx.x / gridDim.x, hi = a.n * (blockIdx.x + 1) / gridDim.x;
+  for (uint64_t base = lo; base < hi; base += span)
   {
     LossGeo<Model> geo[kLossPairs];
     LossSample smp[kLossPairs];
@@ -950,7 +946,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
     for (int k = 0; k < kLossPairs; ++k)
     {
       const uint64_t i = base + uint64_t(k) * kBlock + threadIdx.x;
-      live[k] = i < a.n;
+      live[k] = i < hi;
       if (!live[k]) continue;
       v3 in, out;
       if (a.pairs[0] != nullptr)
@@ -963,20 +959,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
       smp[k] = loss_prepare(a.loss_kind, in, out, ref);
       geo[k].init(in, out);
     }
-    for (int j = 0; j < a.nprobes; ++j)
+    for (int j0 = 0; j0 < a.nprobes; j0 += kLossProbeUnroll)
     {
-      const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(j) * kLossModelBytes);
-      double acc = 0.0;
+      double acc[kLossProbeUnroll];
 #pragma unroll
-      for (int k = 0; k < kLossPairs; ++k)
+      for (int u = 0; u < kLossProbeUnroll; ++u)
       {
-        if (!live[k]) continue;
-        float rgb[3];
-        geo[k].eval(m, a.component, rgb);
-        acc += double(sample_loss(a.loss_kind, smp[k], rgb));
+        acc[u] = 0.0;
+        if (j0 + u >= a.nprobes) break;             // uniform
+        const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(j0 + u) * kLossModelBytes);
+#pragma unroll
+        for (int k = 0; k < kLossPairs; ++k)
+        {
+          if (!live[k]) continue;
+          float rgb[3];
+          geo[k].eval(m, a.component, rgb);
+          acc[u] += double(sample_loss(a.loss_kind, smp[k], rgb));
+        }
       }
-      acc = wave_sum(acc);
-      if (lane == 0) part[wave * a.nprobes + j] += acc;
+#pragma unroll
+      for (int u = 0; u < kLossProbeUnroll; ++u)
+      {
+        if (j0 + u >= a.nprobes) break;
+        const double v = wave_sum(acc[u]);
+        if (lane == 0) part[wave * a.nprobes + j0 + u] += v;
+      }
     }
   }
   __syncthreads();
@@ -987,6 +994,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
     for (int w = 0; w < kBlock / 64; ++w) t += part[w * a.nprobes + j];
     a.block_sums[size_t(blockIdx.x) * a.nprobes + j] = t;
   }
+}
+
+// Workgroups of `kernel` (kBlock threads, `lds` bytes of dynamic LDS) resident on the current device at once (0 if
+// the runtime cannot say)
+template<class K>
+inline uint64_t resident_blocks(K kernel, size_t lds)
+{
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess) return 0;
+  return uint64_t(cus) * uint64_t(per_cu > 0 ? per_cu : 0);
 }
 
 // sums[p] = sum over blocks of block_sums[b][p], in block order (one workgroup per probe; fixed tree)
@@ -1002,9 +1021,15 @@ int launch_loss(const LossArgs& a0, hipStream_t s)
   const size_t lds = size_t(kBlock / 64) * size_t(a.nprobes) * sizeof(double);
   if (kLossPairMajor && lds <= 48 * 1024)       // up to 1536 probes; more take the probe-batch kernel
   {
-    blocks = (a.n + uint64_t(kBlock) * kLossPairs - 1) / (uint64_t(kBlock) * kLossPairs);
+    // as many workgroups as there are passes of kLossPairs samples per thread, up to kLossMaxBlocks; beyond one
+    // device-full of resident workgroups, a whole number of device-fulls (each workgroup then takes an equal
+    // contiguous share), so the last round is not a partial one (measured on config 5: 2 048 workgroups at 768
+    // resident ran 2.67 rounds)
+    const uint64_t need = (a.n + uint64_t(kBlock) * kLossPairs - 1) / (uint64_t(kBlock) * kLossPairs);
+    blocks = need < uint64_t(kLossMaxBlocks) ? need : uint64_t(kLossMaxBlocks);
+    const uint64_t res = resident_blocks(k_loss_pairs<Model>, lds);
+    if (res > 0 && blocks > res) blocks = res * (blocks / res);
     if (blocks < 1) blocks = 1;
-    if (blocks > kLossMaxBlocks) blocks = kLossMaxBlocks;
     hipLaunchKernelGGL((k_loss_pairs<Model>), dim3(unsigned(blocks)), dim3(kBlock), lds, s, a);
   }
   else

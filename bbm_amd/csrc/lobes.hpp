@@ -140,7 +140,7 @@ struct PhongLobe
   {
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
     const float cosA = fmaxf(dot3(mk3(-in.x, -in.y, in.z), out), 0.0f);
-    const float pw = powf_fast(cosA, s);
+    const float pw = powf_ref(cosA, s);
     const float f = (s + 2) * kInvPiHalfF * pw;
     rgb[0] = active ? albedo[0] * f : 0.0f;
     rgb[1] = active ? albedo[1] * f : 0.0f;
@@ -196,7 +196,7 @@ struct Lafortune
     if (MODE & kModeEval)
     {
       const bool active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
-      const float fr = powf_fast(fmaxf(dot3(mk3(cx, cy, cz), mk3(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0f), s);
+      const float fr = powf_ref(fmaxf(dot3(mk3(cx, cy, cz), mk3(in.x * out.x, in.y * out.y, in.z * out.z)), 0.0f), s);
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {
@@ -211,7 +211,7 @@ struct Lafortune
       const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
       const v3 co = normalize3(mk3(cx * out.x, cy * out.y, cz * out.z));
       const float cosA = fmaxf(dot3(co, in), 0.0f);
-      const float p = div_nr(s + 1, kPi2F) * powf_fast(cosA, s);
+      const float p = div_nr(s + 1, kPi2F) * powf_ref(cosA, s);
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;
@@ -317,7 +317,7 @@ struct AshikhminShirley
       exponent = su;
       normalization = f_div_d(double(su) + 1.0, double(kPi2F));
     }
-    const float p = div_nr(normalization * powf_fast(h.z, exponent), 4.0f * hdi);
+    const float p = div_nr(normalization * powf_ref(h.z, exponent), 4.0f * hdi);
     return active ? p : 0.0f;
   }
 
@@ -345,7 +345,7 @@ struct AshikhminShirley
         exponent = su;
         normalization = div_nr(su + 1, kPi8F);
       }
-      const float np = normalization * powf_fast(h.z, exponent);
+      const float np = normalization * powf_ref(h.z, exponent);
       float diff_scale = 0.0f;
       if constexpr (FULL)
       {

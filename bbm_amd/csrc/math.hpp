@@ -51,6 +51,21 @@ template<class M> constexpr bool has_geo()
   else return false;
 }
 
+// Models with an exact-mode evaluation (bbm_hip_set_exact_subnormals: Microfacet over Beckmann's subnormal quotients,
+// Bagher's NDF by glibc's powf / expf, aggregates of such children -- Model::kHasExact) get a second instantiation
+// of the eval kernels, launched while the mode is on (kernels.hpp).
+template<class Model> constexpr bool model_has_exact()
+{
+  if constexpr (requires { Model::kHasExact; }) return Model::kHasExact;
+  else return false;
+}
+template<int MODE, bool EXACT, class Model>
+__device__ __forceinline__ void model_eval_pdf(const Model& m, v3 in, v3 out, uint32_t comp, float* rgb, float& pdf)
+{
+  if constexpr (EXACT && model_has_exact<Model>()) m.template eval_pdf<MODE, true>(in, out, comp, rgb, pdf);
+  else m.template eval_pdf<MODE>(in, out, comp, rgb, pdf);
+}
+
 __device__ __forceinline__ v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 __device__ __forceinline__ v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
 
@@ -519,7 +534,7 @@ __device__ __forceinline__ float erff_glibc(float x)
 // fix-ups with pi_lo.  Not correctly rounded, hence restated rather than rounded from a double atan2.  Same float as
 // this machine's libm on 6e7 random pairs (unit-vector components, any finite floats, mixed magnitudes) and on every
 // combination of zeros, infinities and NaN, and at x = 1 (glibc's atanf shortcut, the same float) for every 13th y
-// (oracle/atan2f_glibc_check.c).  Branch-free: selects around two IEEE divisions.
+// (oracle/atan2f_glibc_check.c).  Selects around two IEEE divisions.
 namespace fdlibm_atan {
 constexpr float kHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
 constexpr float kLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
@@ -669,6 +684,19 @@ __device__ __forceinline__ float powf_fast(float x, float y)
   const float t0 = y * __builtin_amdgcn_logf(x);
   if (__builtin_fabsf(t0) <= 8.0f && x >= 1.17549435e-38f) return __builtin_amdgcn_exp2f(t0);
   return powf_acc(x, y);
+}
+
+// bbm::pow of two floats where the result is a model's value factor (Phong / Lafortune / Ashikhmin-Shirley lobes,
+// the Phong NDF): glibc's powf to its last bit by default; -DBBM_HIP_POWF_FAST (A/B): the ~1e-6 powf_fast
+__device__ __forceinline__ float powf_fast(float x, float y);
+__device__ __forceinline__ float powf_glibc(float x, float y);
+__device__ __forceinline__ float powf_ref(float x, float y)
+{
+#ifdef BBM_HIP_POWF_FAST
+  return powf_fast(x, y);
+#else
+  return powf_glibc(x, y);
+#endif
 }
 
 // x^y for x >= 0 (or NaN), y finite: the float nearest exp2(y log2 x) with y log2 x formed in double to ~2^-40,

@@ -161,7 +161,7 @@ struct PhongNdf
   __device__ __forceinline__ float eval(v3 h) const
   {
     const float normalization = div_nr(sharpness + 2, float(2.0f * kPiD));
-    const float D = powf_fast(h.z, sharpness) * normalization;   // h.z <= 0 lanes are selected away
+    const float D = powf_ref(h.z, sharpness) * normalization;    // h.z <= 0 lanes are selected away
     return (h.z > 0) ? D : 0.0f;
   }
   __device__ __forceinline__ float G1(v3 v, v3 m) const

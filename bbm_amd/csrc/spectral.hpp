@@ -124,7 +124,10 @@ struct Bagher
     return g;
   }
 
-  // eval (Specular component) at a prepared pair
+  // eval (Specular component) at a prepared pair; EXACT (exact mode): the NDF's power and exponential by glibc's own
+  // powf / expf, so D is the reference's float -- Bagher and Aggregate(Lambertian, Bagher) then bit-identical on
+  // nearly every lane, for +68 % kernel time (profiles/r04_ab_bagher_exact_d.txt)
+  template<bool EXACT = false>
   __device__ __forceinline__ void eval_geo(Geo& g, uint32_t component, float* rgb) const
   {
     const bool active = (component & kFlagSpecular) && g.sdirs;
@@ -139,28 +142,33 @@ struct Bagher
       // exp(-t) / t^p: powf_fast (~1e-6) instead of the 173-instruction library powf.  Next to that factor the
       // glibc-exact expf buys nothing (bit-exact lanes 68.9 -> 69.7 %) and cost 12 % (0.162 -> 0.183 ms per
       // 10 M pairs, tools/gpu_r03_e.sh): expf_dn here
-#ifdef BBM_HIP_BAGHER_EXACT_D
-      const float den = powf_glibc(t, p[j]);
-      const float P22 = (den > kEpsF) ? div_nr(expf_glibc_neg(-t), den) : 0.0f;
-#else
-      const float den = powf_fast(t, p[j]);
-      const float P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
-#endif
+      float P22;
+      if constexpr (EXACT)
+      {
+        const float den = powf_glibc(t, p[j]);
+        P22 = (den > kEpsF) ? div_nr(expf_glibc_neg(-t), den) : 0.0f;
+      }
+      else
+      {
+        const float den = powf_fast(t, p[j]);
+        P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
+      }
       const float Dj = ((g.h.z > 0) ? f_div_d(double(P22), g.dnorm) : 0.0f) * K[j];
       const float Gj = g.gmask ? G1q(j, g.q_in, g.th_in) * G1q(j, g.q_out, g.th_out) : 0.0f;
       // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
       const float S = float(double(F0[j]) + double(1.0f - F0[j]) * g.x5);
       const float Fj = S - F1[j] * g.cosF;
-      const float res = eval_scale<Norm::Cook>((Dj * Gj) * Fj, g.zz);
+      const float res = eval_scale<Norm::Cook, EXACT>((Dj * Gj) * Fj, g.zz);
       rgb[j] = active ? res * albedo[j] : 0.0f;
     }
   }
 
-  template<int MODE>
+  static constexpr bool kHasExact = true;
+  template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     Geo g = geometry(in, out);
-    if (MODE & kModeEval) eval_geo(g, component, rgb);
+    if (MODE & kModeEval) eval_geo<EXACT>(g, component, rgb);
     else rgb[0] = rgb[1] = rgb[2] = 0.0f;
     if (MODE & kModePdf)
     {

@@ -15,7 +15,15 @@ try:
 except Exception:
     print(0)")
   if [ $rc -ne 3 ] && [ "$nothing_ran" != 1 ]; then exit $rc; fi
-  echo "[retry] nothing ran (rc=$rc), attempt $i; waiting 60 s"
-  sleep 60
+  # honour the pool's own back-off hint ("retry in Ns"), at least 90 s
+  wait_s=$(python3 -c "
+import json, re
+try:
+    m = re.search(r'retry in (\\d+)s', json.load(open('gpurun_out/.last_call.json')).get('msg', '') or '')
+    print(max(90, int(m.group(1)) + 15) if m else 90)
+except Exception:
+    print(90)")
+  echo "[retry] nothing ran (rc=$rc), attempt $i; waiting $wait_s s"
+  sleep "$wait_s"
 done
 exit 3
