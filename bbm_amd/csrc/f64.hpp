@@ -72,115 +72,9 @@ __device__ __forceinline__ double tan_theta(d3 v) { return sqrt(sin_theta2(v)) /
 __device__ __forceinline__ double tan_theta2(d3 v) { return sin_theta2(v) / (v.z * v.z); }   // spherical.h:186
 __device__ __forceinline__ double safe_sqrt(double a) { return sqrt((a < 0.0) ? 0.0 : a); }
 
-// ---------------------------------------------------------------- exp / log / pow in double
-//
-// The reference's doubleRGB exp / log / pow are glibc's (correctly rounded, or within ~0.52 ulp).  ocml's f64 pow
-// carries its logarithm in double-double and is the bulk of the pow-heavy models' VALU per pair; these
-// restatements stay within a few ulp of glibc at about half the cost (tools/f64math_probe.hip measures them
-// against the host libm), far inside the doubleRGB bar (1e-10 relative, tests/test_gpu_f64.py).
-//
-// 2^f - 1 for |f| <= 1/2: f (c1 + f (c2 + ... c13)), the degree-13 Taylor polynomial of e^(f ln2) - 1
-// (truncation <= 1e-17 relative); no 1 is added, so 2^f - 1 keeps its relative precision as f -> 0
-__device__ __forceinline__ double exp2m1_poly(double f)
-{
-  double p = 0x1.816193166d0f9p-40;
-  p = __builtin_fma(p, f, 0x1.c3bd650fc2986p-36);
-  p = __builtin_fma(p, f, 0x1.e8cac7351bb25p-32);
-  p = __builtin_fma(p, f, 0x1.e4cf5158b8ecap-28);
-  p = __builtin_fma(p, f, 0x1.b5253d395e7c4p-24);
-  p = __builtin_fma(p, f, 0x1.62c0223a5c824p-20);
-  p = __builtin_fma(p, f, 0x1.ffcbfc588b0c7p-17);
-  p = __builtin_fma(p, f, 0x1.430912f86c787p-13);
-  p = __builtin_fma(p, f, 0x1.5d87fe78a6731p-10);
-  p = __builtin_fma(p, f, 0x1.3b2ab6fba4e77p-7);
-  p = __builtin_fma(p, f, 0x1.c6b08d704a0c0p-5);
-  p = __builtin_fma(p, f, 0x1.ebfbdff82c58fp-3);
-  p = __builtin_fma(p, f, 0x1.62e42fefa39efp-1);
-  return p * f;
-}
+// exp / log / pow in double (exp2m1_poly, exp2_d, exp_d, log2_d, exp_lib, log_d, pow_d): math.hpp, shared with the
+// floatRGB exact mode
 
-// 2^t over the whole double range: n = rint(t), 2^(t - n) (t - n exact) scaled by 2^n in one rounding, subnormal
-// results included; overflow to inf, 0 far below 2^-1074, NaN propagates
-__device__ __forceinline__ double exp2_d(double t)
-{
-  const double n = __builtin_rint(t);
-  const double r = __builtin_ldexp(1.0 + exp2m1_poly(t - n), int(__builtin_fmin(__builtin_fmax(n, -1100.0), 1100.0)));
-  return (t < -1100.0) ? 0.0 : ((t > 1100.0) ? __builtin_inf() : r);
-}
-
-// e^a: n = rint(a / ln2), r = a - n ln2 in two FMAs (Cody-Waite; n ln2_hi exact), e^r - 1 by its degree-13
-// Taylor polynomial on |r| <= 0.35 (truncation 1e-17): ~1 ulp over the whole range, subnormal results included
-__device__ __forceinline__ double exp_d(double a)
-{
-#ifdef BBM_HIP_F64_OCML
-  return exp(a);   // A/B: the device library (tools/build_variant.sh)
-#endif
-  const double n = __builtin_rint(a * 0x1.71547652b82fep0);
-  double r = __builtin_fma(-n, 0x1.62e42fefa3800p-1, a);
-  r = __builtin_fma(-n, 0x1.ef35793c76730p-45, r);
-  double p = 1.0 / 6227020800.0;                         // 1 / 13!
-  p = __builtin_fma(p, r, 1.0 / 479001600.0);
-  p = __builtin_fma(p, r, 1.0 / 39916800.0);
-  p = __builtin_fma(p, r, 1.0 / 3628800.0);
-  p = __builtin_fma(p, r, 1.0 / 362880.0);
-  p = __builtin_fma(p, r, 1.0 / 40320.0);
-  p = __builtin_fma(p, r, 1.0 / 5040.0);
-  p = __builtin_fma(p, r, 1.0 / 720.0);
-  p = __builtin_fma(p, r, 1.0 / 120.0);
-  p = __builtin_fma(p, r, 1.0 / 24.0);
-  p = __builtin_fma(p, r, 1.0 / 6.0);
-  p = __builtin_fma(p, r, 0.5);
-  p = __builtin_fma(p, r, 1.0);
-  const double v = __builtin_ldexp(__builtin_fma(p, r, 1.0), int(__builtin_fmin(__builtin_fmax(n, -1100.0), 1100.0)));
-  return (a < -746.0) ? 0.0 : ((a > 710.0) ? __builtin_inf() : v);
-}
-
-// log2(x) for finite x > 0 (subnormals included) to ~1 ulp + 2^-53 absolute: x = 2^k m with m in [1/sqrt2, sqrt2),
-// l0 = v_log_f32(m) (|l0| <= 1/2, 2^-23 relative), one Newton step on 2^L = m: e = m 2^-l0 - 1
-// = (m - 1)(1 + q) + q with q = 2^-l0 - 1 (|e| < 2^-21; m - 1 exact), L = l0 + log2(1 + e) by three terms.
-// Near x = 1 (k = 0) the result keeps its relative precision.
-__device__ __forceinline__ double log2_d(double x)
-{
-  double m = __builtin_amdgcn_frexp_mant(x);             // [1/2, 1)
-  int k = __builtin_amdgcn_frexp_exp(x);
-  const bool lo = m < 0.70710678118654752;
-  m = lo ? m + m : m;
-  k = lo ? k - 1 : k;
-  const float l0 = __builtin_amdgcn_logf(float(m));
-  const double q = exp2m1_poly(-double(l0));
-  const double e = __builtin_fma(m - 1.0, 1.0 + q, q);
-  const double l1p = e * __builtin_fma(e, __builtin_fma(e, 1.0 / 3.0, -0.5), 1.0);
-  return double(k) + __builtin_fma(l1p, 0x1.71547652b82fep0, double(l0));
-}
-
-// the device library's f64 exp: measured faster than exp_d inside the He family's prelude (He 1.50 -> 1.47,
-// HeHolzschuch 0.80 -> 0.75 ms per 10 M pairs; exp_d is faster in the microfacet models: CookTorrance 0.158 ->
-// 0.150), where the kernel runs at its 256-VGPR cap
-__device__ __forceinline__ double exp_lib(double a) { return exp(a); }
-
-// glibc's log restated on log2_d (x < 0 -> NaN; x = 0 -> -inf; inf -> inf; NaN -> NaN)
-__device__ __forceinline__ double log_d(double x)
-{
-#ifdef BBM_HIP_F64_OCML
-  return log(x);
-#endif
-  const double v = log2_d(x) * 0x1.62e42fefa39efp-1;
-  return (x == 0.0) ? -__builtin_inf() : ((x < 0.0) ? __builtin_nan("") : ((x == __builtin_inf()) ? x : v));
-}
-// x^y for x >= 0 (or NaN) and finite y: 2^(y log2 x), y log2 x to ~2^-52 relative + |y| 2^-53 absolute (~1e-13
-// relative on every result above the subnormal range); pow(x, 0) = pow(1, y) = 1, pow(0, y) = 0 / inf,
-// pow(inf, y) = inf / 0, x < 0 -> NaN (never reached: the reference's bases here are >= 0)
-__device__ __forceinline__ double pow_d(double x, double y)
-{
-#ifdef BBM_HIP_F64_OCML
-  return pow(x, y);
-#endif
-  double r = exp2_d(y * log2_d(x));
-  const bool big = x == __builtin_inf();
-  r = (x == 0.0 || big) ? (((y > 0.0) == big) ? __builtin_inf() : 0.0) : r;
-  r = (x < 0.0) ? __builtin_nan("") : r;
-  return (y == 0.0 || x == 1.0) ? 1.0 : r;
-}
 // x^5 for the Schlick / Bagher / Ashikhmin-Shirley factors (1 - c)^5, as glibc's pow(x, 5.0) rounds it: the
 // power carried as a double-double through three exact products (two FMA residuals each), rounded once -- the
 // correctly rounded x^5 but within ~2^-45 ulp of a midpoint.  These factors feed the reflectance weights that

@@ -796,6 +796,29 @@ __global__ __launch_bounds__(64) void k_loss_models(LossArgs a)
   __builtin_memcpy(a.models + size_t(p) * kLossModelBytes, &m, sizeof(Model));
 }
 
+// The wave's sum of a double, computed in registers: four DPP row shifts (v_mov_b32_dpp on both halves, zero
+// outside the row) leave each 16-lane row's sum in its lane 15, and the four row sums are added in row order --
+// a fixed tree, like wave_sum's butterfly, at VALU latency instead of six LDS-crossbar round trips (ds_bpermute)
+template<int CTRL>
+__device__ __forceinline__ double dpp_row(double v)
+{
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int lane)
+{
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane), __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+__device__ __forceinline__ double wave_sum_dpp(double v)
+{
+  v += dpp_row<0x111>(v);     // row_shr:1
+  v += dpp_row<0x112>(v);     // row_shr:2
+  v += dpp_row<0x114>(v);     // row_shr:4
+  v += dpp_row<0x118>(v);     // row_shr:8 -> lane 15 of each row holds the row's sum
+  return ((readlane_d(v, 15) + readlane_d(v, 31)) + readlane_d(v, 47)) + readlane_d(v, 63);
+}
+
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -981,7 +1004,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
       for (int u = 0; u < kLossProbeUnroll; ++u)
       {
         if (j0 + u >= a.nprobes) break;
-        const double v = wave_sum(acc[u]);
+#ifdef BBM_HIP_LOSS_SHFL
+        const double v = wave_sum(acc[u]);     // A/B: the ds_bpermute butterfly
+#else
+        const double v = wave_sum_dpp(acc[u]);
+#endif
         if (lane == 0) part[wave * a.nprobes + j0 + u] += v;
       }
     }

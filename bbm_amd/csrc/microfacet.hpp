@@ -210,6 +210,7 @@ struct StudentT
     f23 = F23(gamma);
   }
 
+  template<bool EXACT = false>
   __device__ __forceinline__ float eval(v3 h) const
   {
     const float alpha2 = (1.0f * au) * av;
@@ -218,8 +219,12 @@ struct StudentT
     const float sn = sqnorm2(div_nr(h.x, au), div_nr(h.y, av));
     // pow(1 + tan^2 / ((gamma - 1) alpha^2), gamma): the reference rounds a double pow; powf_fast is within
     // ~1e-6 of it (the transcendental unit where |gamma log2 x| <= 8, a double exponent beyond) instead of 227
-    // f64 instructions
-    const float den = powf_fast(float(1.0 + div_nr(sn, (gamma - 1) * pow2f(h.z))), gamma);
+    // f64 instructions.  EXACT (exact mode): the double power itself (f64::pow_d, ~1e-13), rounded to float --
+    // the reference's float but within ~2^-19 ulp of a rounding midpoint
+    const float q = div_nr(sn, (gamma - 1) * pow2f(h.z));
+    float den;
+    if constexpr (EXACT) den = float(f64::pow_d(1.0 + double(q), double(gamma)));
+    else den = powf_fast(float(1.0 + q), gamma);
     const float D = div_nr(1.0f, normalization * den);
     return (h.z > 0) ? D : 0.0f;
   }
@@ -394,10 +399,14 @@ struct LowNdf
     norm_pdf = kInvPiHalfF * normalization;
   }
 
+  template<bool EXACT = false>
   __device__ __forceinline__ float eval(v3 h) const
   {
-    // pow(1 + B (1 - z), -C) in double in the reference; powf_fast: within ~1e-6
-    const float S = powf_fast(float(1.0 + B * (1.0 - h.z)), -C);
+    // pow(1 + B (1 - z), -C) in double in the reference; powf_fast: within ~1e-6; EXACT (exact mode): the double
+    // power (f64::pow_d) of the double base, rounded to float
+    float S;
+    if constexpr (EXACT) S = float(f64::pow_d(1.0 + double(B) * (1.0 - double(h.z)), -double(C)));
+    else S = powf_fast(float(1.0 + B * (1.0 - h.z)), -C);
     return (h.z > 0) ? S : 0.0f;
   }
 

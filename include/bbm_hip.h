@@ -64,8 +64,9 @@ const char* bbm_hip_last_error(void);
  * normalisation, the pdf's 1 / (4 |o.h|)) with a double remainder step, so eval and pdf are the reference's floats
  * bit for bit on every lane (ndf/beckmann.h:60 -> glibc expf, microfacet.h:100, :171), at +3.6-4.3 % kernel time on
  * the headline.  Also Bagher's NDF (ndf/sgd.h:56-62: pow(temp, p) and exp(-temp) as glibc's own powf / expf instead
- * of ~1e-6 approximations; +68 % Bagher kernel time), and every fused Aggregate(Lambertian, X) whose X has an exact
- * mode.  Off: those quotients use the f32 remainder step and Bagher's D the fast power; outputs may differ in the
+ * of ~1e-6 approximations; +68 % Bagher kernel time), the Low and Student-T NDFs' double pow (ndf/low.h:53,
+ * ndf/studentt.h:53: LowMicrofacet(Fit), Ribardiere) computed in double and rounded to float, and every fused
+ * Aggregate(Lambertian, X) whose X has an exact mode.  Off: those quotients use the f32 remainder step and Bagher's D the fast power; outputs may differ in the
  * last bits (the per-lane parity bar holds either way).  Returns the previous setting (0 / 1), or a negative code. */
 int bbm_hip_set_exact_subnormals(int on);
 
