@@ -39,8 +39,10 @@ MAX_SAMPLER_FRAC = 0.05       # ... a sampler-CDF proof (a CDF entry moves the ~
 # HOW MUCH): the ill-conditioned lanes of the cancelling models -- Bagher's shadowing 1 + Lambda (1 - e^(c t^k))
 # and the He family's series at tiny D -- reach ~1e-2 at their fitted parameters (profiles/r02_parity_large_0*.json);
 # every other model stays below 1e-3.  A kernel regression confined to ill-conditioned lanes would exceed these.
-EXCUSED_REL_CEILING = {"Bagher": 5e-2, "Aggregate<Lambertian,Bagher>": 5e-2, "He": 2e-2, "HeWestin": 2e-2,
-                       "HeHolzschuch": 2e-2, "NganHe": 2e-2, "Aggregate<Lambertian,NganHe>": 2e-2}
+# round 3: Bagher / Aggregate(Lambertian, Bagher) 5e-2, the He family 2e-2; round 4 (glibc powf / expf / logf / erfcf
+# restated, the measured tail: Bagher 2.9e-3, Aggregate(Lambertian, Bagher) 1.6e-2 on one lane where the Lambertian
+# and a negative Bagher Fresnel term cancel, HeWestin 2.3e-4): the He family under the default ceiling
+EXCUSED_REL_CEILING = {"Bagher": 5e-3, "Aggregate<Lambertian,Bagher>": 2e-2}
 EXCUSED_REL_DEFAULT = 1e-3
 
 
