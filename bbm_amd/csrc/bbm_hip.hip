@@ -579,6 +579,7 @@ __global__ __launch_bounds__(kBlock) void k_libm(int func, const float* a, const
       case BBM_HIP_LIBM_SINF: { float c; sincosf_glibc(x, &r, &c); } break;
       case BBM_HIP_LIBM_COSF: { float sn; sincosf_glibc(x, &sn, &r); } break;
       case BBM_HIP_LIBM_ATAN2F: r = atan2f_glibc(x, b[i]); break;
+      case BBM_HIP_LIBM_THETA: r = theta_of(mk3(x, 0.0f, b[i])); break;
       default: r = erfcf_glibc(x); break;
     }
     out[i] = r;
@@ -1078,9 +1079,9 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
 int bbm_hip_libm_eval(int func, const float* a, const float* b, float* out, size_t n, void* stream)
 {
   if (n == 0) return BBM_HIP_OK;
-  if (func < BBM_HIP_LIBM_EXPF || func > BBM_HIP_LIBM_ATAN2F)
+  if (func < BBM_HIP_LIBM_EXPF || func > BBM_HIP_LIBM_THETA)
     return fail(BBM_HIP_ERR_INVALID_ARG, "unknown libm function");
-  if (!a || !out || ((func == BBM_HIP_LIBM_POWF || func == BBM_HIP_LIBM_ONE_PLUS_SQRT || func == BBM_HIP_LIBM_ATAN2F) && !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "pointer is NULL");
+  if (!a || !out || ((func == BBM_HIP_LIBM_POWF || func == BBM_HIP_LIBM_ONE_PLUS_SQRT || func == BBM_HIP_LIBM_ATAN2F || func == BBM_HIP_LIBM_THETA) && !b)) return fail(BBM_HIP_ERR_INVALID_ARG, "pointer is NULL");
   uint64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
   hipLaunchKernelGGL(k_libm, dim3(unsigned(blocks)), dim3(kBlock), 0, static_cast<hipStream_t>(stream), func, a, b, out,

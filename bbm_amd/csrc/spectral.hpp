@@ -21,13 +21,53 @@ namespace bbmhip {
 // by the reference in double and returned as float; for z < 0, Pi - that.  theta_of keeps that (the
 // linearizers, checkBsdf binning and the Bagher shadowing term use it -- the latter is so ill-conditioned
 // for published fits that a 1-ulp different theta moves G by 1e-2, so theta is rounded from f64 as there).
+//
+// The double asin as a short polynomial: y = |v - pole| / 2 lies in [0, sqrt2 / 2]; asin y = y + y z P(z), z = y^2,
+// for y <= 1/2, and pi/2 - 2 asin s with s = sqrt((1 - y) / 2) <= 1/2 above (w = (1 - y) / 2 exact in double).  P is
+// the asin series economised on Chebyshev nodes over z in [0, 1/4] to degree 11 (truncation 2^-49 of P, well below
+// double rounding once scaled by z / 6; coefficients from exact rational arithmetic, tools/asin_poly.py): the result
+// is within a few double ulps of glibc's asin.  Its float is the reference's unless the double lies within 256 ulps of
+// a float rounding midpoint (~1e-6 of the lanes, and any NaN): those take the device library's double asin, as
+// before.  ~20 f64 VALU against ~70 f64 + ~60 other for the library asin.
+namespace asin_poly {
+constexpr double kP[12] = {
+    0x1.555555555554ep-3, 0x1.3333333337110p-4, 0x1.6db6db68067fep-5,
+    0x1.f1c71fb700f11p-6, 0x1.6e8b26f89d407p-6, 0x1.1c598c739143cp-6,
+    0x1.c86b17413a7b6p-7, 0x1.8559b6cfd3c89p-7, 0x1.fd4f1fa1ac91cp-8,
+    0x1.084522a849f25p-6, -0x1.65717d3785d18p-7, 0x1.cf6d7d2572a46p-6};
+__device__ __forceinline__ double eval(double z)
+{
+  double p = kP[11];
+#pragma unroll
+  for (int k = 10; k >= 0; --k) p = __builtin_fma(p, z, kP[k]);
+  return p;
+}
+}  // namespace asin_poly
+
 __device__ __forceinline__ float theta_of(v3 v)
 {
   const float sz = (v.z < 0.0f) ? -1.0f : 1.0f;          // bbm::sign = copysign(1, z)
   const float dz = v.z - sz;
   const float nrm = sqrtf(((0.0f + v.x * v.x) + v.y * v.y) + dz * dz);
-  const double t = 2.0 * asin(0.5 * double(nrm));
-  return (v.z >= 0) ? float(t) : float(double(kPiF) - t);
+  const double y = 0.5 * double(nrm);
+  const bool hi = y > 0.5;
+  const double w = hi ? (1.0 - y) * 0.5 : y * y;
+  // sqrt(w) for the upper range (w in [0.146, 0.25]): rsq seed, two Newton steps (~2^-90 before rounding)
+  const double g = __builtin_amdgcn_rsq(w);
+  double sq = w * g;
+  sq = __builtin_fma(__builtin_fma(-sq, sq, w), 0.5 * g, sq);
+  sq = __builtin_fma(__builtin_fma(-sq, sq, w), 0.5 * g, sq);
+  const double s = hi ? sq : y;
+  const double r = __builtin_fma(s * w, asin_poly::eval(w), s);
+  const double t = 2.0 * (hi ? 0x1.921fb54442d18p+0 - 2.0 * r : r);
+  double u = (v.z >= 0) ? t : double(kPiF) - t;
+  const uint32_t lo = uint32_t(__builtin_bit_cast(uint64_t, u)) & 0x1fffffffu;
+  if (__builtin_expect(((lo - 0x0fffff00u) < 0x200u) || (u != u), false))
+  {
+    const double te = 2.0 * asin(y);
+    u = (v.z >= 0) ? te : double(kPiF) - te;
+  }
+  return float(u);
 }
 
 struct Bagher

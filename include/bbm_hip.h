@@ -463,7 +463,7 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
 
 /* The device restatements of the host libm float functions the reference's native backbone calls (glibc 2.35's
  * expf, logf, powf, erff, erfcf, sinf, cosf, atan2f: bbm_amd/csrc/math.hpp), evaluated elementwise on n device floats:
- * out[i] = f(a[i]) (f(a[i], b[i]) for powf, ONE_PLUS_SQRT, atan2f; b may be NULL otherwise).  For pinning them against the host libm on
+ * out[i] = f(a[i]) (f(a[i], b[i]) for powf, ONE_PLUS_SQRT, atan2f, THETA; b may be NULL otherwise).  For pinning them against the host libm on
  * the machine that runs the reference (tests/test_gpu_libm.py); not on any BSDF path. */
 #define BBM_HIP_LIBM_EXPF 0
 #define BBM_HIP_LIBM_LOGF 1
@@ -474,6 +474,7 @@ int bbm_hip_sphere_dirs(const float* xi0, const float* xi1, size_t n, int hemisp
 #define BBM_HIP_LIBM_SINF 6
 #define BBM_HIP_LIBM_COSF 7
 #define BBM_HIP_LIBM_ATAN2F 8       /* atan2f(a, b) */
+#define BBM_HIP_LIBM_THETA 9        /* spherical::theta of the direction (a, 0, b): float(2 asin(|v - pole| / 2)) */
 int bbm_hip_libm_eval(int func, const float* a, const float* b, float* out, size_t n, void* stream);
 
 #ifdef __cplusplus

@@ -13,7 +13,7 @@ from tests import oracle_util as ou
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4, "one_plus_sqrt": 5, "sinf": 6, "cosf": 7, "atan2f": 8}
+FUNCS = {"expf": 0, "logf": 1, "powf": 2, "erff": 3, "erfcf": 4, "one_plus_sqrt": 5, "sinf": 6, "cosf": 7, "atan2f": 8, "theta": 9}
 
 
 @pytest.fixture(scope="module")
@@ -132,3 +132,24 @@ def test_atan2f_bitexact(lib):
     got, want = _device(lib, "atan2f", a, b), _host("atan2f", a, b)
     bad = np.nonzero(~_same(got, want))[0]
     assert bad.size == 0, f"{bad.size} lanes differ, e.g. y={a[bad[:4]]} x={b[bad[:4]]} got={got[bad[:4]]} libm={want[bad[:4]]}"
+
+
+def test_theta_bitexact(lib):
+    """theta_of (spectral.hpp: spherical::theta by a polynomial double asin with a midpoint guard) against numpy's
+    IEEE double arcsin of the same float chord, rounded to float as the reference does: random unit and near-pole
+    directions in both hemispheres, every lane bit-identical."""
+    rng = np.random.default_rng(20261021)
+    n = 1 << 22
+    v = rng.normal(size=(2, n))
+    v /= np.linalg.norm(v, axis=0)
+    x = np.concatenate([v[0], rng.uniform(-1e-3, 1e-3, n // 4), [0, 1, -1, 0.70710678]]).astype(np.float32)
+    z = np.concatenate([v[1], np.sign(rng.uniform(-1, 1, n // 4)) * np.sqrt(1 - 1e-6), [1, 0, 0, 0.70710678]]).astype(np.float32)
+    got = _device(lib, "theta", x, z)
+    f = np.float32
+    sz = np.where(z < 0, f(-1), f(1))
+    dz = (z - sz).astype(f)
+    nrm = np.sqrt(((f(0) + x * x) + f(0) * f(0)) + dz * dz).astype(f)
+    te = 2.0 * np.arcsin(0.5 * nrm.astype(np.float64))
+    want = np.where(z >= 0, te, np.float64(np.float32(np.pi)) - te).astype(f)
+    bad = np.nonzero(~_same(got, want))[0]
+    assert bad.size == 0, f"{bad.size} lanes differ, e.g. x={x[bad[:4]]} z={z[bad[:4]]} got={got[bad[:4]]} want={want[bad[:4]]}"
