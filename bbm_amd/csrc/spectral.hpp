@@ -44,6 +44,13 @@ __device__ __forceinline__ double eval(double z)
 }
 }  // namespace asin_poly
 
+// the guard's fallback, out of line: the library asin's registers would otherwise count against every kernel
+__device__ __attribute__((noinline)) inline double theta_lib(double y, bool below)
+{
+  const double te = 2.0 * asin(y);
+  return below ? double(kPiF) - te : te;
+}
+
 __device__ __forceinline__ float theta_of(v3 v)
 {
   const float sz = (v.z < 0.0f) ? -1.0f : 1.0f;          // bbm::sign = copysign(1, z)
@@ -62,11 +69,7 @@ __device__ __forceinline__ float theta_of(v3 v)
   const double t = 2.0 * (hi ? 0x1.921fb54442d18p+0 - 2.0 * r : r);
   double u = (v.z >= 0) ? t : double(kPiF) - t;
   const uint32_t lo = uint32_t(__builtin_bit_cast(uint64_t, u)) & 0x1fffffffu;
-  if (__builtin_expect(((lo - 0x0fffff00u) < 0x200u) || (u != u), false))
-  {
-    const double te = 2.0 * asin(y);
-    u = (v.z >= 0) ? te : double(kPiF) - te;
-  }
+  if (__builtin_expect(((lo - 0x0fffff00u) < 0x200u) || (u != u), false)) u = theta_lib(y, !(v.z >= 0));
   return float(u);
 }
 
