@@ -546,8 +546,14 @@ __device__ __forceinline__ float atan_pos(float x)
 {
   const uint32_t ix = __float_as_uint(x);
   const int id = (ix < 0x3f300000u) ? 0 : ((ix < 0x3f980000u) ? 1 : ((ix < 0x401c0000u) ? 2 : 3));
-  const float num = (id == 0) ? 2.0f * x - 1.0f : ((id == 1) ? x - 1.0f : ((id == 2) ? x - 1.5f : -1.0f));
-  const float den = (id == 0) ? 2.0f + x : ((id == 1) ? x + 1.0f : ((id == 2) ? 1.0f + 1.5f * x : x));
+  // num = a x + b, den = c x + d with the reference's roundings (a x exact for a in {0, 1, 2}; 1.5 x rounded, then
+  // + 1): constant selects and two products, no per-lane branches
+  const float a = (id == 0) ? 2.0f : ((id == 3) ? 0.0f : 1.0f);
+  const float b = (id == 0) ? -1.0f : ((id == 2) ? -1.5f : -1.0f);
+  const float c = (id == 2) ? 1.5f : 1.0f;
+  const float d = (id == 0) ? 2.0f : ((id == 3) ? 0.0f : 1.0f);
+  const float num = a * x + b;
+  const float den = c * x + d;
   const bool small = ix < 0x3ee00000u;                           // |x| < 0.4375: no reduction
   const float t = small ? x : __fdiv_rn(num, den);
   const float z = t * t;
@@ -576,7 +582,9 @@ __device__ __forceinline__ float atan2f_glibc(float y, float x)
   z = (k > 60) ? pi_o_2 + 0.5f * pi_lo : ((xneg && k < -60) ? 0.0f : z);
   float r = (m == 0) ? z : ((m == 1) ? -z : ((m == 2) ? pi - (z - pi_lo) : (z - pi_lo) - pi));
   // (glibc's x = 1 shortcut, atanf(y), is this same float: y / 1 = y, |y| >= 2^25 -> hi + lo = pi_o_2 + pi_lo / 2)
-  // infinities and zeros
+  // infinities, zeros and NaN on a wave-uniform branch: a direction's components are finite and almost never 0
+  const bool special = (ix - 1u >= 0x7f7fffffu) || (iy - 1u >= 0x7f7fffffu);
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(special) == 0, true)) return r;
   r = (iy == 0x7f800000u) ? (yneg ? -pi_o_2 : pi_o_2) : r;
   const float xinf = (iy == 0x7f800000u) ? ((m == 0) ? pi_o_4 : (m == 1) ? -pi_o_4 : (m == 2) ? 3.0f * pi_o_4 : -3.0f * pi_o_4)
                                          : ((m == 0) ? 0.0f : (m == 1) ? -0.0f : (m == 2) ? pi : -pi);
