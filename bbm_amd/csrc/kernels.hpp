@@ -928,13 +928,13 @@ template<class Model> struct LossGeo<Model, false>
 // row; the block's rows are summed in wave order at the end.  Against the probe-batch kernel below (k_loss): the
 // decode runs once per call instead of once per 12-probe batch, and register pressure no longer grows with the batch.
 #ifndef BBM_HIP_LOSS_PAIRS
-#define BBM_HIP_LOSS_PAIRS 2
+#define BBM_HIP_LOSS_PAIRS 1
 #endif
 #ifndef BBM_HIP_LOSS_PAIRS_WAVES
-#define BBM_HIP_LOSS_PAIRS_WAVES 3
+#define BBM_HIP_LOSS_PAIRS_WAVES 4
 #endif
 #ifndef BBM_HIP_LOSS_PROBE_UNROLL
-#define BBM_HIP_LOSS_PROBE_UNROLL 1
+#define BBM_HIP_LOSS_PROBE_UNROLL 2
 #endif
 constexpr int kLossPairs = BBM_HIP_LOSS_PAIRS;
 constexpr int kLossProbeUnroll = BBM_HIP_LOSS_PROBE_UNROLL;   // probes evaluated per iteration of the probe loop
@@ -944,9 +944,10 @@ constexpr bool kLossPairMajor = false;       // A/B: the probe-batch kernel k_lo
 #else
 constexpr bool kLossPairMajor = true;
 #endif
-// minimum waves per SIMD of k_loss_pairs; measured on config 5 (profiles/r04_ab_fit_loss_kernel.txt): 2 pairs per
-// thread at 3 waves 0.607-0.610 ms per compass step, 1 pair at 3 waves 0.626-0.632, unconstrained (2 waves, 218
-// VGPRs) 0.79-0.81, the probe-batch kernel 0.654-0.656.  The He family keeps the compiler's choice (models.hpp).
+// minimum waves per SIMD of k_loss_pairs; measured on config 5 (profiles/r04_ab_fit_loss_kernel*.txt, ms per compass
+// step, interleaved on one box): 1 pair x 2 probes per iteration at 4 waves 0.599-0.601, 1 x 4 at 4 waves 0.603-0.607,
+// 1 x 4 / 1 x 2 / 2 x 2 / 2 x 1 at 3 waves 0.67-0.70 (0.607-0.610 for 2 x 1 on an earlier box), unconstrained (2 waves,
+// 218 VGPRs) 0.79-0.81, the probe-batch kernel 0.654-0.656.  The He family keeps the compiler's choice (models.hpp).
 template<class Model> struct loss_pair_waves { static constexpr int value = BBM_HIP_LOSS_PAIRS_WAVES; };
 template<class Model>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pair_waves<Model>::value, 8))) void k_loss_pairs(LossArgs a)
