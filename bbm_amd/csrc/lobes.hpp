@@ -484,7 +484,9 @@ struct LowSmooth
   }
   __device__ __forceinline__ static double pow2d(double x) { return x * x; }
 
-  template<int MODE>
+  // exact mode (bbm_hip_set_exact_subnormals): S's double power computed in double (f64::pow_d), rounded to float
+  static constexpr bool kHasExact = true;
+  template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     const bool active = (component & kFlagSpecular) && (in.z >= 0) && (out.z >= 0);
@@ -492,7 +494,9 @@ struct LowSmooth
     {
       const float dp2 = sqnorm2(in.x + out.x, in.y + out.y);
       const float cosD = float(safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y)));
-      const float S = powf_fast(float(1.0 + B * dp2), -C);     // double pow in the reference; see LowNdf::eval
+      float S;                                                  // double pow in the reference; see LowNdf::eval
+      if constexpr (EXACT) S = float(f64::pow_d(1.0 + double(B * dp2), -double(C)));   // B Dp2 is a float product
+      else S = powf_fast(float(1.0 + B * dp2), -C);
       const float Q = fres.eval(cosD);
 #pragma unroll
       for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0f;

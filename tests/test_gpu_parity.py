@@ -305,7 +305,7 @@ def test_exact_subnormal_mode_is_bit_exact(bbm, mode_in, mode_out):
 
 # exact mode beyond the Beckmann quotients: model -> bit-identical fraction it must reach on every parameter set
 EXACT_MODE_FLOOR = {"Bagher": 0.999, "Aggregate<Lambertian,Bagher>": 0.999, "LowMicrofacet": 0.999,
-                    "LowMicrofacetFit": 0.999, "Ribardiere": 0.0}
+                    "LowMicrofacetFit": 0.999, "Ribardiere": 0.0, "LowSmooth": 0.999}
 
 
 @pytest.mark.parametrize("name", list(EXACT_MODE_FLOOR))
