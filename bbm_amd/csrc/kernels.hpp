@@ -933,6 +933,11 @@ template<class Model> struct LossGeo<Model, false>
 #ifndef BBM_HIP_LOSS_PAIRS_WAVES
 #define BBM_HIP_LOSS_PAIRS_WAVES 4
 #endif
+// where k_loss_pairs reads a probe's model: 0 by reference in global memory (scalar loads at each use), 1 a copy by
+// value (bulk scalar loads, SGPR spills to VGPR lanes), 2 staged in LDS at kernel start (broadcast LDS reads)
+#ifndef BBM_HIP_LOSS_MODEL
+#define BBM_HIP_LOSS_MODEL 0
+#endif
 #ifndef BBM_HIP_LOSS_PROBE_UNROLL
 #define BBM_HIP_LOSS_PROBE_UNROLL 2
 #endif
@@ -953,9 +958,18 @@ template<class Model>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pair_waves<Model>::value, 8))) void k_loss_pairs(LossArgs a)
 {
   static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
-  extern __shared__ double part[];                       // [kBlock / 64][nprobes]
+  extern __shared__ double part[];                       // [kBlock / 64][nprobes] (+ the models, BBM_HIP_LOSS_MODEL 2)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int j = threadIdx.x; j < (kBlock / 64) * a.nprobes; j += kBlock) part[j] = 0.0;
+#if BBM_HIP_LOSS_MODEL == 2
+  constexpr int kLdsModelBytes = (int(sizeof(Model)) + 15) & ~15;
+  char* mlds = reinterpret_cast<char*>(part + (kBlock / 64) * a.nprobes);
+  for (int w = threadIdx.x; w < a.nprobes * (kLdsModelBytes / 4); w += kBlock)
+  {
+    const int j = w / (kLdsModelBytes / 4), o = w % (kLdsModelBytes / 4);
+    reinterpret_cast<uint32_t*>(mlds)[w] = reinterpret_cast<const uint32_t*>(a.models + size_t(j) * kLossModelBytes)[o];
+  }
+#endif
   __syncthreads();
   // this workgroup's contiguous share of the samples: equal to one sample per thread and pass across the grid, so
   // no workgroup runs an extra pass the others do not (the grid is a multiple of the resident workgroups)
@@ -991,7 +1005,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pai
       {
         acc[u] = 0.0;
         if (j0 + u >= a.nprobes) break;             // uniform
+#if BBM_HIP_LOSS_MODEL == 2
+        const Model& m = *reinterpret_cast<const Model*>(mlds + size_t(j0 + u) * kLdsModelBytes);
+#elif BBM_HIP_LOSS_MODEL == 1
+        const Model m = *reinterpret_cast<const Model*>(a.models + size_t(j0 + u) * kLossModelBytes);
+#else
         const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(j0 + u) * kLossModelBytes);
+#endif
 #pragma unroll
         for (int k = 0; k < kLossPairs; ++k)
         {
@@ -1046,7 +1066,10 @@ int launch_loss(const LossArgs& a0, hipStream_t s)
   LossArgs a = a0;
   hipLaunchKernelGGL((k_loss_models<Model>), dim3(unsigned((a.nprobes + 63) / 64)), dim3(64), 0, s, a);
   uint64_t blocks;
-  const size_t lds = size_t(kBlock / 64) * size_t(a.nprobes) * sizeof(double);
+  size_t lds = size_t(kBlock / 64) * size_t(a.nprobes) * sizeof(double);
+#if BBM_HIP_LOSS_MODEL == 2
+  lds += size_t(a.nprobes) * ((sizeof(Model) + 15) & ~size_t(15));
+#endif
   if (kLossPairMajor && lds <= 48 * 1024)       // up to 1536 probes; more take the probe-batch kernel
   {
     // as many workgroups as there are passes of kLossPairs samples per thread, up to kLossMaxBlocks; beyond one

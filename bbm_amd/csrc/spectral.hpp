@@ -45,7 +45,7 @@ __device__ __forceinline__ double eval(double z)
 }  // namespace asin_poly
 
 // the guard's fallback, out of line: the library asin's registers would otherwise count against every kernel
-__device__ __attribute__((noinline)) inline double theta_lib(double y, bool below)
+__device__ __attribute__((noinline, pure)) inline double theta_lib(double y, bool below)
 {
   const double te = 2.0 * asin(y);
   return below ? double(kPiF) - te : te;
@@ -117,7 +117,7 @@ struct Bagher
   // 1 + Lambda (1 - exp(c d^k)) out of line: the exact powf / expf hold ~40 VGPRs of f64 temporaries, and inlined
   // into each of the six (channel, direction) branches they set the register budget of every kernel around them
   // (the loss kernel spilled 124 VGPRs instead of 69) although at the default theta0 = pi/2 no lane takes them
-  __device__ __attribute__((noinline)) static float g1_tail(float d, float c, float k, float Lambda)
+  __device__ __attribute__((noinline, pure)) static float g1_tail(float d, float c, float k, float Lambda)
   {
     return 1.0f + Lambda * (1.0f - expf_glibc(c * powf_glibc(d, k)));
   }
