@@ -112,11 +112,15 @@ __device__ __forceinline__ void wave_reduce_check(double* acc)
   }
 }
 
-template<class Model, int TEST>
+// minimum waves per SIMD of the checkBsdf kernels: 4 (<= 128 VGPRs) -- the glibc-exact erff / logf / expf of the
+// Beckmann VNDF took the CookTorrance importance-sampling kernel to 161 VGPRs (3 waves) when left to the compiler,
+// at 4 it needs no spills; the He family and EPD spill at 4 and keep the compiler's choice (models.hpp)
 #ifndef BBM_HIP_CHECK_WAVES
-#define BBM_HIP_CHECK_WAVES 1
+#define BBM_HIP_CHECK_WAVES 4
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BBM_HIP_CHECK_WAVES, 8))) void k_check(CheckArgs a)
+template<class Model> struct check_waves { static constexpr int value = BBM_HIP_CHECK_WAVES; };
+template<class Model, int TEST>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(check_waves<Model>::value, 8))) void k_check(CheckArgs a)
 {
   __shared__ double part[kBlock / 64][kCheckAcc];
   const Model m(a.p.v);

@@ -25,6 +25,10 @@ template<class B> struct eval_grid_cap<Aggregate<Lambertian, B>> { static conste
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
 template<class B> struct loss_pair_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_pair_waves<B>::value; };
+template<class B> struct check_waves<Aggregate<Lambertian, B>> { static constexpr int value = check_waves<B>::value; };
+template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
+struct check_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
+template<> struct check_waves<EpdM> { static constexpr int value = 1; };
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct loss_pair_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
 // Bagher's evaluation holds ~180 VGPRs (two waves per SIMD) unconstrained.  Measured (10M pairs, eval+pdf,
