@@ -121,3 +121,16 @@ def test_parse_model_matches_fromstring(bbm, s):
             return ("*", m.runtime, [flat(c) for c in m._children])
         return (m.name, m.model_id, m.runtime, m.parameter_values().tolist())
     assert flat(bbm.parse_model(s)) == flat(bbm.fromString(s))
+
+
+def test_fit_material_through_the_c_parser(bbm):
+    """Config 5's material comes from the fits/ line itself (tools/bench_configs.FIT_LINE, fits/bagher_sgd.fit:3)
+    parsed by the library's C parser, and equals the reference's fromString of that line (tests/golden/fits.json)."""
+    import json
+    import os
+    from tools import bench_configs
+    name, m = bench_configs.fit_material()
+    assert name == "alum-bronze" and m.name == "Aggregate<Lambertian,Bagher>" and m.runtime
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fits.json")) as f:
+        row = next(r for r in json.load(f)["bagher_sgd.fit"] if r[0] == name)
+    assert np.array_equal(m.parameter_values(), bbm.fromString(row[1]).parameter_values())
