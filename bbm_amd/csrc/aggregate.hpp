@@ -133,4 +133,6 @@ struct Aggregate
   }
 };
 
+template<class A, class B> struct exact_sample<Aggregate<A, B>> { using type = Aggregate<exact_sample_t<A>, exact_sample_t<B>>; };
+
 }  // namespace bbmhip

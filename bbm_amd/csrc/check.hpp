@@ -286,6 +286,30 @@ inline uint32_t check_blocks(uint64_t n, int nslots)
 // partials [nslots][nblocks][kCheckAcc] -> acc [nslots][kCheckAcc] (fixed order; defined in bbm_hip.hip)
 __global__ __launch_bounds__(kBlock) void k_check_final(const double* partial, int nblocks, double* acc);
 
+// one test's kernel for model type K; SAMPLING: only the tests that call the model's sampler (importance-sampled
+// reflectance, pdf, sample-pdf, sample count) -- the exact-sampling twin needs no other instantiation.  false: no such test.
+template<class K, bool SAMPLING>
+bool launch_check_kernel(int test, dim3 grid, const CheckArgs& a, hipStream_t s)
+{
+  switch (test)
+  {
+    case kCheckReflectance: hipLaunchKernelGGL((k_check<K, kCheckReflectance>), grid, dim3(kBlock), 0, s, a); return true;
+    case kCheckPdf: hipLaunchKernelGGL((k_check<K, kCheckPdf>), grid, dim3(kBlock), 0, s, a); return true;
+    case kCheckSamplePdf: hipLaunchKernelGGL((k_check<K, kCheckSamplePdf>), grid, dim3(kBlock), 0, s, a); return true;
+    case kCheckSampleCount: hipLaunchKernelGGL((k_check<K, kCheckSampleCount>), grid, dim3(kBlock), 0, s, a); return true;
+    default: break;
+  }
+  if constexpr (!SAMPLING)
+    switch (test)
+    {
+      case kCheckReciprocity: hipLaunchKernelGGL((k_check<K, kCheckReciprocity>), grid, dim3(kBlock), 0, s, a); return true;
+      case kCheckAdjoint: hipLaunchKernelGGL((k_check<K, kCheckAdjoint>), grid, dim3(kBlock), 0, s, a); return true;
+      case kCheckPdfInt: hipLaunchKernelGGL((k_check<K, kCheckPdfInt>), grid, dim3(kBlock), 0, s, a); return true;
+      default: break;
+    }
+  return false;
+}
+
 template<class Model>
 int launch_check(int test, const CheckArgs& a0, double* acc, hipStream_t s)
 {
@@ -297,17 +321,11 @@ int launch_check(int test, const CheckArgs& a0, double* acc, hipStream_t s)
   struct Release { void* p; hipStream_t s; ~Release() { host_params<Model>::done(p, s); } } release{scratch, s};
   const uint32_t bx = check_blocks(a.n, a.nslots);
   const dim3 grid(bx, unsigned(a.nslots));
-  switch (test)
-  {
-    case kCheckReflectance: hipLaunchKernelGGL((k_check<Model, kCheckReflectance>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckReciprocity: hipLaunchKernelGGL((k_check<Model, kCheckReciprocity>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckAdjoint: hipLaunchKernelGGL((k_check<Model, kCheckAdjoint>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckPdf: hipLaunchKernelGGL((k_check<Model, kCheckPdf>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckPdfInt: hipLaunchKernelGGL((k_check<Model, kCheckPdfInt>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckSamplePdf: hipLaunchKernelGGL((k_check<Model, kCheckSamplePdf>), grid, dim3(kBlock), 0, s, a); break;
-    case kCheckSampleCount: hipLaunchKernelGGL((k_check<Model, kCheckSampleCount>), grid, dim3(kBlock), 0, s, a); break;
-    default: return fail(BBM_HIP_ERR_INVALID_ARG, "unknown check test");
-  }
+  bool launched = false;
+  if constexpr (has_exact_sample<Model>())       // exact mode: the sampler's twin with glibc's erff / logf (math.hpp)
+    if (exact_subnormals().load() != 0) launched = launch_check_kernel<exact_sample_t<Model>, true>(test, grid, a, s);
+  if (!launched && !launch_check_kernel<Model, false>(test, grid, a, s))
+    return fail(BBM_HIP_ERR_INVALID_ARG, "unknown check test");
   if (test != kCheckSampleCount)
     hipLaunchKernelGGL(k_check_final, dim3(unsigned(a.nslots)), dim3(64), 0, s, a.partial, int(bx), acc);
   const hipError_t e = hipGetLastError();

@@ -694,7 +694,17 @@ int launch_sample_mask(const SampleArgs& a0, hipStream_t s)
   uint64_t blocks = (units + kBlock - 1) / kBlock;
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks()) blocks = max_blocks();
-  if (vec) hipLaunchKernelGGL((k_sample_v4<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+  bool twin = false;
+  if constexpr (has_exact_sample<Model>())       // exact mode: the sampler's twin with glibc's erff / logf (math.hpp)
+    if (exact_subnormals().load() != 0)
+    {
+      using T = exact_sample_t<Model>;
+      if (vec) hipLaunchKernelGGL((k_sample_v4<T, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_sample_v1<T, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
+      twin = true;
+    }
+  if (twin) {}
+  else if (vec) hipLaunchKernelGGL((k_sample_v4<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   else hipLaunchKernelGGL((k_sample_v1<Model, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(BBM_HIP_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(e));

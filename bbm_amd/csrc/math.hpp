@@ -59,6 +59,13 @@ template<class Model> constexpr bool model_has_exact()
   if constexpr (requires { Model::kHasExact; }) return Model::kHasExact;
   else return false;
 }
+// The samplers' exact-mode twin: a model type whose sampler reproduces glibc's float erff / logf where the default
+// uses the device library's (Beckmann's visible-normal sampler, microfacet.hpp), launched by the sample and
+// checkBsdf kernels while the mode is on.  Same parameters and layout; identity for every other model.
+template<class M> struct exact_sample { using type = M; };
+template<class M> using exact_sample_t = typename exact_sample<M>::type;
+template<class M> constexpr bool has_exact_sample() { return !__is_same(exact_sample_t<M>, M); }
+
 template<int MODE, bool EXACT, class Model>
 __device__ __forceinline__ void model_eval_pdf(const Model& m, v3 in, v3 out, uint32_t comp, float* rgb, float& pdf)
 {

@@ -25,8 +25,9 @@ __device__ __forceinline__ float erfinv_s(float a)
 #endif
 }
 
-// ndf::beckmann<CONF, Symmetry, Normalize> (include/ndf/beckmann.h:40-213)
-template<bool Aniso, bool Normalize>
+// ndf::beckmann<CONF, Symmetry, Normalize> (include/ndf/beckmann.h:40-213).  ExactSample: the exact-mode twin
+// (exact_sample_t below), whose sampler reproduces glibc's erff / logf
+template<bool Aniso, bool Normalize, bool ExactSample = false>
 struct Beckmann
 {
   static constexpr int kParams = Aniso ? 2 : 1;
@@ -70,12 +71,25 @@ struct Beckmann
     if (!((xi0 >= 0) && (xi1 >= 0) && (xi0 <= 1) && (xi1 <= 1))) return mk3(0.0f, 0.0f, 0.0f);
     const v3 vs = normalize3(mk3(view.x * au, view.y * av, view.z));
     const float tanT = tan_theta(vs);
-    // erf, log and exp of floats: glibc's erff / logf / expf restated bit for bit (math.hpp), so the Newton
-    // iteration starts from and converges to the reference's own floats
-    const float maxval = erff_glibc(div_nr(1.0f, tanT));
+    // erf and log of floats: in the exact twin glibc's erff / logf restated bit for bit (math.hpp), so the Newton
+    // iteration starts from the reference's own float -- 28 % of a CookTorrance importance sample (three divergent
+    // erff branches per wave, 2.19 vs 1.70 ms per 125 M samples, profiles/r04_ab_sample_vndf.txt); by default the
+    // device library's erff / logf (<= 2 ulp), from which the three Newton steps land on the reference's direction
+    // on all but ~1e-5 of the lanes (the rest within the input-ulps proof, tests/test_gpu_parity.py)
+    const float tc = div_nr(1.0f, tanT);
     float xc0 = clampf(xi0, float(10e-6), float(1.0 - 10e-6));
     const float xc1 = clampf(xi1, float(10e-6), float(1.0 - 10e-6));
-    float x = maxval - (maxval + 1) * erff_glibc(sqrtf(-logf_glibc(xc0)));
+    float maxval, x;
+    if constexpr (ExactSample)
+    {
+      maxval = erff_glibc(tc);
+      x = maxval - (maxval + 1) * erff_glibc(sqrtf(-logf_glibc(xc0)));
+    }
+    else
+    {
+      maxval = erff(tc);
+      x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
+    }
     xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_glibc_neg(-(vs.z * vs.z))));
     for (int i = 0; i < 3; ++i)
     {
@@ -613,5 +627,10 @@ struct Microfacet
     flag = kFlagSpecular;
   }
 };
+
+template<bool A, bool N> struct exact_sample<Beckmann<A, N>> { using type = Beckmann<A, N, true>; };
+template<class NDF, class MS, class FRESNEL, Norm N, bool Scaled>
+struct exact_sample<Microfacet<NDF, MS, FRESNEL, N, Scaled>>
+{ using type = Microfacet<exact_sample_t<NDF>, MS, FRESNEL, N, Scaled>; };
 
 }  // namespace bbmhip

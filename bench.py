@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--models", default=None, help="comma-separated subset of models for --workload models|sample "
                                                    "(counter passes profile one model at a time)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--no-exact", action="store_true", help="evalpdf: skip the exact-subnormal mode's timing")
+    ap.add_argument("--no-exact", action="store_true", help="evalpdf, sample: skip the exact mode's timing")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="evalpdf: time the K steps as HIP-graph replays of R launches (K/R replays, R | K) instead of "

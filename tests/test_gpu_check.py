@@ -85,6 +85,45 @@ def test_reflectance_matches_reference(chk, name, importance):
             _close(acc[t, c], want[c], scale, 2e-5 if importance else 1e-5, f"{name} theta {t} ch {c}")
 
 
+@pytest.mark.parametrize("test", ["reflectance", "pdf", "count"])
+def test_exact_sampling_twin_matches_reference(chk, test):
+    """Exact mode launches the sampling tests on the sampler's twin (glibc erff / logf in Beckmann's visible-normal
+    sampler, math.hpp exact_sample_t): importance-sampled reflectance, the pdf test and the sample histogram still
+    equal the reference's to the same bars as the default sampler."""
+    bbm, check = chk
+    m = _model(bbm, "CookTorrance")
+    p = m.parameter_values()
+    bbm.set_exact_subnormals(True)
+    try:
+        if test == "reflectance":
+            n = 200_000
+            outs = check.reflectance_outs(3)
+            acc = check.run(m, check.REFLECTANCE, n, 3, torch.from_numpy(outs).cuda(), SEED, importance=True)
+            for t in range(3):
+                want = co.reflectance("CookTorrance", p, outs[:, t], n, SEED, t, True)
+                assert abs(acc[t, 3] - want[3]) <= 2
+                scale = max(abs(want[:3]).max(), 1e-12)
+                for c in range(3):
+                    _close(acc[t, c], want[c], scale, 2e-5, f"exact theta {t} ch {c}")
+        elif test == "pdf":
+            n = 100_000
+            acc = check.run(m, check.PDF, n, 1, None, SEED, sphere=False)[0]
+            for j, (neg, below, mism) in enumerate(co.pdf_test("CookTorrance", p, n, SEED, False)):
+                assert acc[j] == neg and abs(acc[2 + j] - below) <= 2
+                assert abs(acc[4 + j] - mism) <= 1e-3 * mism + 1e-5 * n
+        else:
+            th, ph, trials, ns = 6, 10, 2, 50_000
+            t = check.trial_directions(check.SAMPLE_COUNT, SEED, trials)
+            counts = check.run(m, check.SAMPLE_COUNT, ns, trials, t, SEED, bins=(th, ph))
+            tn = t.cpu().numpy()
+            for k in range(trials):
+                wc = co.sample_count("CookTorrance", p, tn[:, k], k, ns, SEED, th, ph)
+                assert counts[k].sum() == wc.sum()
+                assert np.abs(counts[k] - wc).sum() <= max(2, 1e-3 * wc.sum()), (counts[k], wc)
+    finally:
+        bbm.set_exact_subnormals(False)
+
+
 @pytest.mark.parametrize("name", MODELS)
 @pytest.mark.parametrize("test", [1, 2])
 def test_reciprocity_and_adjoint_match_reference(chk, name, test):

@@ -565,6 +565,39 @@ def test_sample_large_batch_vs_reference(bbm):
     _report("sample_large", stats)
 
 
+BECKMANN_SAMPLERS = ("CookTorrance", "CookTorranceWalter", "CookTorranceHeitz", "NganCookTorrance")
+
+
+@pytest.mark.parametrize("name", BECKMANN_SAMPLERS)
+def test_exact_mode_sampling(bbm, name):
+    """Exact mode's sampler twin (math.hpp exact_sample_t): Beckmann's visible-normal sampler starts its Newton
+    steps from glibc's erff / logf (the default: the device library's).  Both modes meet the bar or the proofs on
+    the 1M-sample batch; the twin's directions are within 1e-6 of the reference on at least as many lanes, and the
+    checkBsdf reflectance statistic it feeds equals the default's to Monte-Carlo noise."""
+    n = 1 << 20
+    out = bbm.fill_directions(0xBB5EED, 2, 0, n, mode=1)
+    xi = torch.rand((2, n), generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")
+    hout, hxi = out.cpu().numpy(), xi.cpu().numpy()
+    m = bbm.BsdfModel(name)
+    params = m.parameter_values()
+    ref, rflag = ou.oracle_sample(name, params, hout, hxi, nthreads=8)
+    stats = {}
+    try:
+        for mode in (True, False):
+            bbm.set_exact_subnormals(mode)
+            s = m.sample(out, xi)
+            torch.cuda.synchronize()
+            got = np.concatenate([s.direction.cpu().numpy(), s.pdf.cpu().numpy()[None]], 0)
+            stats["exact" if mode else "default"] = _check_samples(bbm, name, params, hout, hxi, got,
+                                                                   s.flag.cpu().numpy(), ref, rflag, f"{name} {mode}")
+    finally:
+        bbm.set_exact_subnormals(False)
+    ex, de = stats["exact"], stats["default"]
+    assert ex["frac_dir_within_1e-6"] >= de["frac_dir_within_1e-6"], stats
+    assert ex["dir_lanes_outside_bar"] <= de["dir_lanes_outside_bar"], stats
+    _report(f"exact_sample_{name}", stats)
+
+
 def test_cpp_adapter_drop_in(bbm):
     """backbone/hip C++ adapter: the same bbm::bsdfmodel<> instances (reference template API) on the
     CPU (native backbone) and through bbm::hip::{eval_pdf, sample} on the GPU (tests/cpp)."""

@@ -163,6 +163,10 @@ def bench_models(args, dist, rank, world):
               {"scaling": "weak", "per_model": per})
 
 
+# models of config 4 whose sampler has an exact-mode twin (math.hpp exact_sample_t: Beckmann's glibc erff / logf)
+EXACT_SAMPLERS = ("CookTorrance",)
+
+
 def bench_sample(args, dist, rank, world):
     per_gpu = 125_000_000
     slots = 8
@@ -187,11 +191,20 @@ def bench_sample(args, dist, rank, world):
 
         elapsed, kern_ms = _timed(step, args, dist, stream)
         a = check._gather_acc(acc.cpu().numpy(), dist)
+        exact_ms = None
+        if world == 1 and not args.no_exact and name in EXACT_SAMPLERS:
+            # the same steps on the sampler's exact-mode twin (glibc erff / logf in the Beckmann sampler)
+            prev = bbm_amd.set_exact_subnormals(True)
+            try:
+                exact_ms = _timed(step, args, dist, stream)[1]
+            finally:
+                bbm_amd.set_exact_subnormals(prev)
         total = (per_gpu // slots) * slots * world
         est = a[:, :3] / float(total // slots)
         refl = m.reflectance(outs).cpu().numpy().T
         res[name] = {"samples_per_s": total * args.steps / elapsed, "kernel_ms": kern_ms,
                      "samples_per_dispatch": (per_gpu // slots) * slots,
+                     "exact_mode_kernel_ms": exact_ms,
                      "roofline": valu_roofline(f"sample:{name}", kern_ms, (per_gpu // slots) * slots),
                      "estimate_vs_reflectance": [[float(x) for x in est[k]] + [float(y) for y in refl[k]] for k in (0, slots - 1)]}
         total_t += elapsed

@@ -68,6 +68,7 @@ step_pmc() {
       evalpdf) sel=(--model "$M" --pairs "$units" --no-exact --graph off);;
       fit) sel=(--fit-max-steps 0);;
       models) sel=(--models "$M" --graph off);;
+      sample) sel=(--models "$M" --no-exact);;    # the default sampler, not the exact-mode twin timed after it
     esac
     for P in "$SQ8" "$LANE"; do
       local tag

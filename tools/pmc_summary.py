@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs for one kernel: per-dispatch counter sums (median over dispatches).
+"""Summarise rocprofv3 --pmc CSVs for one kernel: per-dispatch counter sums (median over dispatches); when the
+pattern matches several kernels, the one with the longest median dispatch.
 
     python tools/pmc_summary.py gpurun_out/pmc2 k_eval_pdf_v4            # {counter: median, dispatch_ns: ...}
     python tools/pmc_summary.py --by-kernel gpurun_out/pmc2 k_check      # {kernel name: {counter: median, ...}}
@@ -29,7 +30,7 @@ def summarise(root, pattern, by_kernel=False):
             k = r["Kernel_Name"]
             if pattern not in k:
                 continue
-            kk = k if by_kernel else pattern
+            kk = k
             per[(kk, f, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             dur[kk][(f, r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     byc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -40,7 +41,11 @@ def summarise(root, pattern, by_kernel=False):
         out[kk] = {c: statistics.median(v) for c, v in cs.items()}
         out[kk]["dispatch_ns"] = statistics.median(dur[kk].values())
         out[kk]["dispatches"] = len(dur[kk])
-    return out if by_kernel else out.get(pattern, {})
+    if by_kernel:
+        return out
+    # one kernel per summary: the pattern can also match a short companion kernel (k_check -> k_check_final), whose
+    # dispatches must not enter the medians -- the matching kernel with the longest median dispatch is the one
+    return max(out.values(), key=lambda c: c["dispatch_ns"]) if out else {}
 
 
 if __name__ == "__main__":
