@@ -112,8 +112,10 @@ struct Beckmann
   __device__ __forceinline__ float pdf(v3 view, v3 m, float D) const { return vndf_pdf(*this, view, m, D); }
 };
 
-// ndf::ggx<CONF, Symmetry> (include/ndf/ggx.h:37-196)
-template<bool Aniso>
+// ndf::ggx<CONF, Symmetry> (include/ndf/ggx.h:37-196).  ExactSample: the exact-mode twin (exact_sample_t), whose
+// sampler takes glibc's sinf / cosf of the azimuth (the default: the device library's sincosf, <= 1 ulp; 10 % of a
+// GGX importance sample, profiles/r04_ab_sample_sincos.txt)
+template<bool Aniso, bool ExactSample = false>
 struct GGX
 {
   static constexpr int kParams = Aniso ? 2 : 1;
@@ -152,7 +154,8 @@ struct GGX
     const float r = sqrtf(xi0);
     const float phi = float(((xi1 < a) ? double(div_nr(xi1, a)) : 1.0 + ddiv_nr(double(xi1 - a), 1.0 - a)) * kPiF);
     float sp, cp;
-    sincosf_glibc(phi, &sp, &cp);
+    if constexpr (ExactSample) sincosf_glibc(phi, &sp, &cp);
+    else sincosf(phi, &sp, &cp);
     const float P1 = r * cp;
     const float P2 = float(((xi1 < a) ? 1.0 : double(vs.z)) * r * sp);
     const float sq = float(safe_sqrt(1.0 - P1 * P1 - P2 * P2));
@@ -629,6 +632,7 @@ struct Microfacet
 };
 
 template<bool A, bool N> struct exact_sample<Beckmann<A, N>> { using type = Beckmann<A, N, true>; };
+template<bool A> struct exact_sample<GGX<A>> { using type = GGX<A, true>; };
 template<class NDF, class MS, class FRESNEL, Norm N, bool Scaled>
 struct exact_sample<Microfacet<NDF, MS, FRESNEL, N, Scaled>>
 { using type = Microfacet<exact_sample_t<NDF>, MS, FRESNEL, N, Scaled>; };

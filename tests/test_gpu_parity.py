@@ -565,15 +565,15 @@ def test_sample_large_batch_vs_reference(bbm):
     _report("sample_large", stats)
 
 
-BECKMANN_SAMPLERS = ("CookTorrance", "CookTorranceWalter", "CookTorranceHeitz", "NganCookTorrance")
+EXACT_SAMPLERS = ("CookTorrance", "CookTorranceWalter", "CookTorranceHeitz", "NganCookTorrance", "GGX", "GGXHeitz")
 
 
-@pytest.mark.parametrize("name", BECKMANN_SAMPLERS)
+@pytest.mark.parametrize("name", EXACT_SAMPLERS)
 def test_exact_mode_sampling(bbm, name):
     """Exact mode's sampler twin (math.hpp exact_sample_t): Beckmann's visible-normal sampler starts its Newton
-    steps from glibc's erff / logf (the default: the device library's).  Both modes meet the bar or the proofs on
-    the 1M-sample batch; the twin's directions are within 1e-6 of the reference on at least as many lanes, and the
-    checkBsdf reflectance statistic it feeds equals the default's to Monte-Carlo noise."""
+    steps from glibc's erff / logf, GGX's takes glibc's sinf / cosf of the azimuth (the default: the device
+    library's).  Both modes meet the bar or the proofs on the 1M-sample batch, and the twin's directions are within
+    1e-6 of the reference on at least as many lanes (checkBsdf's statistics: tests/test_gpu_check.py)."""
     n = 1 << 20
     out = bbm.fill_directions(0xBB5EED, 2, 0, n, mode=1)
     xi = torch.rand((2, n), generator=torch.Generator(device="cuda").manual_seed(5), device="cuda")

@@ -163,8 +163,9 @@ def bench_models(args, dist, rank, world):
               {"scaling": "weak", "per_model": per})
 
 
-# models of config 4 whose sampler has an exact-mode twin (math.hpp exact_sample_t: Beckmann's glibc erff / logf)
-EXACT_SAMPLERS = ("CookTorrance",)
+# models of config 4 whose sampler has an exact-mode twin (math.hpp exact_sample_t: Beckmann's glibc erff / logf,
+# GGX's glibc sinf / cosf)
+EXACT_SAMPLERS = ("CookTorrance", "GGX")
 
 
 def bench_sample(args, dist, rank, world):
