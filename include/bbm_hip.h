@@ -70,7 +70,8 @@ const char* bbm_hip_last_error(void);
  * the Beckmann visible-normal sampler starts its Newton steps from glibc's erff / logf (ndf/beckmann.h:92-95) and
  * GGX's takes glibc's sinf / cosf of its azimuth (ndf/ggx.h:98) instead of the device library's (+28 % / +7 % on
  * importance-sampled reflectance).  Off: those quotients use the f32 remainder step, Bagher's D the fast power and
- * the samplers the device functions; outputs may differ in the last bits (the per-lane parity bar holds either way).  Returns the previous setting (0 / 1), or a negative code. */
+ * the samplers the device functions; outputs may differ in the last bits (the per-lane parity bar holds either way).
+ * Returns the previous setting (0 / 1), or a negative code. */
 int bbm_hip_set_exact_subnormals(int on);
 
 /* Model registry.  Replaces the compile-time registry of BBM_EXPORT_BSDFMODEL
