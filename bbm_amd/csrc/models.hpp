@@ -34,8 +34,8 @@ struct loss_pair_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED
 // Bagher's fitting loss (config 5) runs at 8 waves per SIMD: 64 VGPRs with ~55 of the per-sample decode state spilled
 // to scratch (read back once per probe pair from L1), against 128 VGPRs and no spills at 4.  The kernel is
 // latency-bound (issue 0.40), so the doubled occupancy outweighs the spill traffic.  Measured on config 5, ms per
-// compass step, interleaved (profiles/r04_ab_fit_loss_waves*.txt): 4 waves 0.591, 5 0.618, 6 0.572, 7 0.588, 8 0.554; at 8 waves 3 or 4 probes
-// per iteration 0.559 / 0.567, the probe models staged in LDS 0.566.
+// compass step, interleaved (profiles/r04_ab_fit_loss_waves*.txt): 4 waves 0.591, 5 0.618, 6 0.572, 7 0.588,
+// 8 0.554; at 8 waves 3 or 4 probes per iteration 0.559 / 0.567, the probe models staged in LDS 0.566.
 #ifndef BBM_HIP_BAGHER_LOSS_WAVES
 #define BBM_HIP_BAGHER_LOSS_WAVES 8
 #endif
