@@ -67,8 +67,8 @@ const char* bbm_hip_last_error(void);
  * of ~1e-6 approximations; +68 % Bagher kernel time), the Low and Student-T NDFs' double pow (ndf/low.h:53,
  * ndf/studentt.h:53: LowMicrofacet(Fit), Ribardiere) computed in double and rounded to float, and every fused
  * Aggregate(Lambertian, X) whose X has an exact mode.  Sampling (bbm_hip_sample, bbm_hip_check's sampling tests):
- * the Beckmann visible-normal sampler starts its Newton steps from glibc's erff / logf (ndf/beckmann.h:92-95) and
- * GGX's takes glibc's sinf / cosf of its azimuth (ndf/ggx.h:98) instead of the device library's (+28 % / +7 % on
+ * the Beckmann visible-normal sampler starts its Newton steps from glibc's erff / logf (ndf/beckmann.h:94-96) and
+ * GGX's takes glibc's sinf / cosf of its azimuth (ndf/ggx.h:99) instead of the device library's (+28 % / +7 % on
  * importance-sampled reflectance).  Off: those quotients use the f32 remainder step, Bagher's D the fast power and
  * the samplers the device functions; outputs may differ in the last bits (the per-lane parity bar holds either way).
  * Returns the previous setting (0 / 1), or a negative code. */
