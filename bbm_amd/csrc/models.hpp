@@ -47,6 +47,12 @@ template<> struct loss_pair_waves<Bagher> { static constexpr int value = BBM_HIP
 #define BBM_HIP_BAGHER_WAVES 3
 #endif
 template<> struct eval_waves<Bagher> { static constexpr int value = BBM_HIP_BAGHER_WAVES; };
+#ifdef BBM_HIP_MERL_WAVES
+template<> struct eval_waves<Merl> { static constexpr int value = BBM_HIP_MERL_WAVES; };   // A/B
+#endif
+#ifdef BBM_HIP_EPD_WAVES
+template<> struct eval_waves<EpdM> { static constexpr int value = BBM_HIP_EPD_WAVES; };   // A/B
+#endif
 
 // Ribardiere's per-thread Student-T setup (two tgamma, a pow): 2048 workgroups (8 per CU, each thread ~5 iterations
 // over 10M pairs) measured 0.139 -> 0.121 ms per 10M-pair eval (1024 / 4096 / 8192: 0.125 / 0.128 / 0.134;
