@@ -98,3 +98,20 @@ def test_cpu_topology_is_consistent():
     threads, phys, smt, quota, _ = bh.cpu_topology()
     assert threads == len(os.sched_getaffinity(0)) and 1 <= phys <= threads and smt >= 1
     assert quota is None or quota > 0
+
+
+def test_pmc_summary_keeps_to_the_longest_matching_kernel(tmp_path):
+    """tools/pmc_summary.py: a pattern that also matches a short companion kernel (k_check -> k_check_final) must not
+    mix the companion's dispatches into the medians -- the summary is the longest matching kernel's."""
+    from tools import pmc_summary
+    rows = ["Kernel_Name,Dispatch_Id,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp"]
+    for d in range(3):
+        rows.append(f'"void k_check<M, 0>(CheckArgs)",{2 * d},SQ_INSTS_VALU,{1000 + d},0,{2_000_000 + d}')
+        rows.append(f'"k_check_final(double const*, int, double*)",{2 * d + 1},SQ_INSTS_VALU,7,0,5000')
+    p = tmp_path / "pass1" / "run"
+    p.mkdir(parents=True)
+    (p / "x_counter_collection.csv").write_text("\n".join(rows) + "\n")
+    s = pmc_summary.summarise(str(tmp_path), "k_check")
+    assert s["SQ_INSTS_VALU"] == 1001 and s["dispatches"] == 3 and s["dispatch_ns"] == 2_000_001
+    both = pmc_summary.summarise(str(tmp_path), "k_check", by_kernel=True)
+    assert len(both) == 2
