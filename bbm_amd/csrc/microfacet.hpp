@@ -90,11 +90,13 @@ struct Beckmann
       maxval = erff(tc);
       x = maxval - (maxval + 1) * erff(sqrtf(-logf(xc0)));
     }
-    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expf_glibc_neg(-(vs.z * vs.z))));
+    // exp of a float: glibc's expf (x <= 0) in the twin, the 1.4-ulp expf_dn by default
+    const auto expn = [](float v) { return ExactSample ? expf_glibc_neg(v) : expf_dn(v); };
+    xc0 = float(xc0 * (1.0 + maxval + kInvSqrtPiF * tanT * expn(-(vs.z * vs.z))));
     for (int i = 0; i < 3; ++i)
     {
       const float slope = erfinv_s(x);
-      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expf_glibc_neg(-slope * slope) - xc0);
+      const float val = float(1.0 + x + kInvSqrtPiF * tanT * expn(-slope * slope) - xc0);
       // float(1.0 - p) of a float p: one double op on float operands rounded to float is the float op itself
       // (53 >= 2 x 24 + 2), so the f32 subtraction -- likewise 2 xc1 - 1 below (2 xc1 exact in either type)
       const float der = 1.0f - slope * tanT;
