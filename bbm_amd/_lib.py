@@ -80,9 +80,19 @@ SIGNATURES = {
     "bbm_hip_check_tree_workspace_size": (_SZ, [_P]),
     "bbm_hip_check_tree": (_I, [_P, _I, _P, _P, _P, _P, _SZ, _P]),
     "bbm_hip_check_tree_f64": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "bbm_hip_rng_init": (_I, [_P, _U64, _U64, _U64]),
+    "bbm_hip_rng_draw": (_I, [_P, _P, _SZ]),
+    "bbm_hip_gather_samples": (_I, [_P, _SZ, _U64, _P, _P, _I, _P]),
+    "bbm_hip_gather_samples_f64": (_I, [_P, _SZ, _U64, _P, _P, _I, _P]),
+    "bbm_hip_comm_unique_id": (_I, [_P, _SZ]),
+    "bbm_hip_comm_init": (_I, [_P, _SZ, _I, _I, _P]),
+    "bbm_hip_comm_destroy": (_I, [_P]),
+    "bbm_hip_comm_rank": (_I, [_P]),
+    "bbm_hip_comm_size": (_I, [_P]),
+    "bbm_hip_allreduce_sums": (_I, [_P, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
 AGGREGATE_BSDF = -101   # BBM_HIP_AGGREGATE_BSDF: a composed runtime aggregate (aggregatebsdf, what fromString builds)
 RUNTIME_AGGREGATE = 0x40000000   # BBM_HIP_RUNTIME_AGGREGATE: OR-ed into a fused aggregate's id -> aggregatebsdf semantics
@@ -99,6 +109,16 @@ class ChildF64(ctypes.Structure):
     """bbm_hip_child_f64: the same with double parameters (doubleRGB)."""
     _fields_ = [("model_id", ctypes.c_int), ("params", ctypes.c_void_p), ("nparams", ctypes.c_int),
                 ("children", ctypes.c_void_p), ("nchildren", ctypes.c_int)]
+
+
+class Rng(ctypes.Structure):
+    """bbm_hip_rng (include/bbm_hip.h): the state of bbm::rng<Size_t> (std::mt19937_64 + uniform_int_distribution)."""
+    _fields_ = [("mt", ctypes.c_uint64 * 312), ("pos", ctypes.c_uint64), ("lower", ctypes.c_uint64),
+                ("upper", ctypes.c_uint64)]
+
+
+COMM_ID_BYTES = 128     # BBM_HIP_COMM_ID_BYTES
+RNG_DEFAULT_SEED = 5489  # BBM_HIP_RNG_DEFAULT_SEED (std::mt19937_64::default_seed)
 
 
 class BackboneError(RuntimeError):

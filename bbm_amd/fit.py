@@ -160,23 +160,38 @@ class SampledLoss:
         self._ws_probes = 0
         self.launches = 0
 
+    def update(self):
+        """sampledlossfunction::update() (sampledlossfunction.h:52): nothing to refresh."""
+
+    def _sample_loss(self, idx, params=None):
+        if not 0 <= idx < self.total:
+            return 0.0
+        return Batch._one(self, idx, params)
+
     def samples(self):
         return self.total
 
-    def _workspace(self, nprobes):
+    def materialized(self):
+        """This rank's shard as (pairs, reference table, n): the pairs computed once if the loss streams them from the
+        linearizer (materialize=False)."""
+        if self.pairs is None:
+            self.pairs = self.lin.directions(self.begin, self.n, self.stream)
+        return self.pairs, self.ref, self.n
+
+    def _workspace(self, nprobes, n=None):
         torch = _torch()
-        if self._ws is None or self._ws_probes < nprobes:
-            lib = _lib.load()
-            nbytes = (lib.bbm_hip_loss_tree_workspace_size(nprobes, self.n) if self.tree
-                      else lib.bbm_hip_loss_workspace_size(nprobes))
+        lib = _lib.load()
+        nbytes = (lib.bbm_hip_loss_tree_workspace_size(nprobes, self.n if n is None else n) if self.tree
+                  else lib.bbm_hip_loss_workspace_size(nprobes))
+        if self._ws is None or self._ws.numel() * 8 < nbytes:
             self._ws = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=self.dev)
             self._ws_probes = nprobes
         return self._ws
 
-    def probe_sums(self, probes):
+    def probe_sums(self, probes, pairs=None, ref=None, n=None):
         """Per-probe loss sums over the WHOLE grid: this rank's shard (local_sums), then the
         cross-rank all-reduce -- RCCL over xGMI, 2P doubles per compass step."""
-        sums = self.local_sums(probes)
+        sums = self.local_sums(probes) if pairs is None else self.local_sums(probes, pairs, ref, n)
         if self.dist is not None and self.dist.get_world_size() > 1:
             torch = _torch()
             stream = getattr(self, "stream", None)
@@ -186,45 +201,55 @@ class SampledLoss:
             self.dist.all_reduce(sums)
         return sums
 
-    def _tree_sums(self, probes):
-        """bbm_hip_loss_tree(_f64): any model, probes on the host."""
+    def _tree_sums(self, probes, pairs=None, ref=None, n=None):
+        """bbm_hip_loss_tree(_f64): any model, probes on the host; over this rank's shard, or over the given pairs /
+        reference table of n samples (a batch's gathered samples)."""
         torch = _torch()
+        if pairs is None:
+            pairs, ref, n = self.pairs, self.ref, self.n
         npar = self.fitted.parameter_values().size
         p = np.ascontiguousarray(np.asarray(probes, dtype=np.float64 if self.f64 else np.float32).reshape(-1, npar))
         nprobes = p.shape[0]
         sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
-        ws = self._workspace(nprobes)
+        if n == 0:
+            return sums.zero_()
+        ws = self._workspace(nprobes, n)
         _on_stream(self.stream, sums, ws)
         tree, ntree, _keep = tree_desc(self.fitted, self.f64)
         lib = _lib.load()
         fn = lib.bbm_hip_loss_tree_f64 if self.f64 else lib.bbm_hip_loss_tree
-        din, dout = self.pairs
-        _lib.check(fn(tree, ntree, p.ctypes.data, npar, nprobes, self.n, din[0].data_ptr(), din[1].data_ptr(),
+        din, dout = pairs
+        _lib.check(fn(tree, ntree, p.ctypes.data, npar, nprobes, n, din[0].data_ptr(), din[1].data_ptr(),
                       din[2].data_ptr(), dout[0].data_ptr(), dout[1].data_ptr(), dout[2].data_ptr(),
-                      self.ref[0].data_ptr(), self.ref[1].data_ptr(), self.ref[2].data_ptr(), self.loss_kind,
+                      ref[0].data_ptr(), ref[1].data_ptr(), ref[2].data_ptr(), self.loss_kind,
                       self.component, self.unit, sums.data_ptr(), ws.data_ptr(), ws.numel() * 8,
                       _stream_ptr(self.stream)))
         self.launches += 1
         return sums
 
-    def local_sums(self, probes):
-        """Per-probe loss sums over this rank's shard: one bbm_hip_loss launch -> float64 tensor (nprobes,)."""
+    def local_sums(self, probes, pairs=None, ref=None, n=None):
+        """Per-probe loss sums over this rank's shard (or over the given pairs / reference table of n samples): one
+        bbm_hip_loss launch -> float64 tensor (nprobes,)."""
         if self.tree:
-            return self._tree_sums(probes)
+            return self._tree_sums(probes, pairs, ref, n)
         torch = _torch()
+        if pairs is None:
+            pairs, ref, n = self.pairs, self.ref, self.n
         p = np.ascontiguousarray(np.asarray(probes, dtype=np.float32).reshape(-1, self.fitted._params.size))
         nprobes, npar = p.shape
         dp = torch.from_numpy(p).to(self.dev, non_blocking=False)
         sums = torch.empty(nprobes, dtype=torch.float64, device=self.dev)
+        if n == 0:
+            return sums.zero_()
         ws = self._workspace(nprobes)
         _on_stream(self.stream, dp, sums, ws)
         lib = _lib.load()
-        if self.pairs is not None:
-            din, dout = self.pairs
-            _lib.check(lib.bbm_hip_loss_pairs(self.fitted.model_id, dp.data_ptr(), npar, nprobes, self.n,
+        if pairs is not None:
+            din, dout = pairs
+            _lib.check(lib.bbm_hip_loss_pairs(self.fitted.model_id, dp.data_ptr(), npar, nprobes, n,
                                               din[0].data_ptr(), din[1].data_ptr(), din[2].data_ptr(),
                                               dout[0].data_ptr(), dout[1].data_ptr(), dout[2].data_ptr(),
-                                              self.ref[0].data_ptr(), self.ref[1].data_ptr(), self.ref[2].data_ptr(),
+                                              ref[0].data_ptr(), ref[1].data_ptr(), ref[2].data_ptr(),
                                               self.loss_kind, self.component, self.unit, sums.data_ptr(), ws.data_ptr(),
                                               ws.numel() * 8, _stream_ptr(self.stream)))
         else:
@@ -241,11 +266,127 @@ class SampledLoss:
         s = self.probe_sums(probes).cpu().numpy()
         return s / float(self.total) if getattr(self, "f64", False) else (s / float(self.total)).astype(np.float32)
 
-    def __call__(self, params=None):
-        """Loss of one parameter vector (the fitted model's current parameters by default)."""
+    def __call__(self, arg=None, params=None):
+        """Loss of one parameter vector `arg` (the fitted model's current parameters by default); with an integer
+        `arg`, the loss of that sample alone (sampledlossfunction::operator()(idx), sampledlossfunction.h:62-73; 0
+        past the last sample) at `params`."""
+        if isinstance(arg, (int, np.integer)):
+            return self._sample_loss(int(arg), params)
+        params = arg if params is None else params
         p = self.fitted.parameter_values() if params is None else params
         f64 = getattr(self, "f64", False)
         return float(self.probe_losses(np.asarray(p, np.float64 if f64 else np.float32)[None])[0])
+
+
+class BatchRng:
+    """bbm::rng<Size_t> (backbone/native/include/backbone/random.h:40-66): std::mt19937_64 and libstdc++'s
+    uniform_int_distribution over [lower, upper] (both ends included), restated in the library (bbm_hip_rng_*) so a
+    batch draws the reference's indices for the same seed."""
+
+    def __init__(self, seed=_lib.RNG_DEFAULT_SEED, lower=0, upper=2 ** 64 - 1):
+        self.state = _lib.Rng()
+        _lib.check(_lib.load().bbm_hip_rng_init(ctypes.byref(self.state), int(seed), int(lower), int(upper)))
+
+    def draw(self, n):
+        """The next n numbers -> (n,) uint64."""
+        out = np.zeros(int(n), np.uint64)
+        _lib.check(_lib.load().bbm_hip_rng_draw(ctypes.byref(self.state), out.ctypes.data, out.size))
+        return out
+
+
+class Batch:
+    """bbm::batch<SAMPLEDLOSSFUNC> (include/bbm/batch.h:27-92): the loss over `batchsize` samples of a SampledLoss,
+    drawn at random (with repetition) and redrawn by every update() -- compass calls update() once per step
+    (compass.h:103), so each step scores its 2P probes on a fresh batch.
+
+    Indices: bbm::rng<Size_t>(seed, 0, samples()) (batch.h:40), i.e. in [0, samples()] -- the last value is past the
+    final sample and that lane's loss is 0 (sampledlossfunction.h:65-66).  The batch's samples are gathered from the
+    materialised pairs and reference table (bbm_hip_gather_samples, one device pass per update) and all probes are
+    scored in one launch of the inner loss's kernel.  Sharded losses (dist): each rank gathers the indices inside its
+    own shard; the per-probe sums are all-reduced as for the whole grid.
+
+    loss_value() / probe_losses(): sum over the batch / batchsize.  The reference's whole-batch operator()
+    (batch.h:75-82) reads an uninitialised loop index (`for(size_t i; ...)`, undefined behaviour); this is the
+    mean it was written to compute.  __call__(idx) is batch::operator()(idx) (batch.h:64-70)."""
+
+    def __init__(self, batchsize, sampledloss, seed=_lib.RNG_DEFAULT_SEED):
+        self.loss = sampledloss
+        self.batchsize = int(batchsize)
+        self.rng = BatchRng(seed, 0, sampledloss.samples())
+        self.f64 = getattr(sampledloss, "f64", False)
+        self.fitted = sampledloss.fitted
+        self.index = np.zeros(self.batchsize, np.uint64)
+        self._gathered = None
+        self.update()
+
+    def update(self):
+        """batch.h:48-54: the wrapped loss's update(), then batchsize fresh indices."""
+        self.loss.update()
+        self.index = self.rng.draw(self.batchsize)
+        self._gathered = None
+
+    def samples(self):
+        return self.batchsize
+
+    def _gather(self, index):
+        """This rank's samples among the global indices `index`, gathered densely -> (pairs, ref, n)."""
+        torch = _torch()
+        pairs, ref, n = self.loss.materialized()
+        begin = self.loss.begin
+        idx = np.asarray(index, np.uint64)
+        mine = idx[(idx >= begin) & (idx < begin + n)] - np.uint64(begin)
+        dt = torch.float64 if self.f64 else torch.float32
+        dst = torch.empty((9, max(mine.size, 1)), dtype=dt, device=ref.device)
+        src = [pairs[0][k] for k in range(3)] + [pairs[1][k] for k in range(3)] + [ref[k] for k in range(3)]
+        src = [t.contiguous() for t in src]
+        sp = (ctypes.c_void_p * 9)(*[t.data_ptr() for t in src])
+        dp = (ctypes.c_void_p * 9)(*[dst[k].data_ptr() for k in range(9)])
+        mine = np.ascontiguousarray(mine)
+        lib = _lib.load()
+        fn = lib.bbm_hip_gather_samples_f64 if self.f64 else lib.bbm_hip_gather_samples
+        _on_stream(self.loss.stream, dst)
+        got = _lib.check(fn(mine.ctypes.data, mine.size, n, ctypes.cast(sp, ctypes.c_void_p),
+                            ctypes.cast(dp, ctypes.c_void_p), 9, _stream_ptr(self.loss.stream)))
+        g = dst[:, :got]
+        return (g[0:3], g[3:6]), g[6:9], int(got)
+
+    def probe_sums(self, probes):
+        """Per-probe loss sums over the current batch (all ranks), one launch -> float64 tensor (nprobes,)."""
+        if self._gathered is None:
+            self._gathered = self._gather(self.index)
+        pairs, ref, n = self._gathered
+        return self.loss.probe_sums(probes, pairs, ref, n)
+
+    def probe_losses(self, probes):
+        """Mean loss over the batch per probe, as Value (float32; float64 in doubleRGB)."""
+        s = self.probe_sums(probes).cpu().numpy()
+        return s / float(self.batchsize) if self.f64 else (s / float(self.batchsize)).astype(np.float32)
+
+    def loss_value(self, params=None):
+        p = self.fitted.parameter_values() if params is None else params
+        return float(self.probe_losses(np.asarray(p, np.float64 if self.f64 else np.float32)[None])[0])
+
+    def __call__(self, arg=None, params=None):
+        """batch::operator()(idx) (batch.h:64-70) for an integer `arg`: the wrapped loss at the idx-th drawn index (0
+        for idx >= batchsize and for the masked index samples()); otherwise the batch mean at parameters `arg`."""
+        if not isinstance(arg, (int, np.integer)):
+            return self.loss_value(arg if params is None else params)
+        if not 0 <= int(arg) < self.batchsize:
+            return 0.0
+        i = int(self.index[int(arg)])
+        return 0.0 if i >= self.loss.samples() else Batch._one(self.loss, i, params)
+
+    @staticmethod
+    def _one(loss, i, params):
+        """The loss of global sample i alone at params, through a one-sample gather (sums over ranks: only the
+        owner's is nonzero)."""
+        p = loss.fitted.parameter_values() if params is None else params
+        g = Batch.__new__(Batch)
+        g.loss, g.f64 = loss, getattr(loss, "f64", False)
+        pairs, ref, n = g._gather(np.asarray([i], np.uint64))
+        dt = np.float64 if g.f64 else np.float32
+        s = loss.probe_sums(np.asarray(p, dt)[None], pairs, ref, n).cpu().numpy()[0]
+        return float(dt(s))
 
 
 class Compass:
@@ -285,9 +426,11 @@ class Compass:
         return self.full.copy()
 
     def reset(self):
-        """compass.h:145-150: step size back to the initial one, loss of the current parameters."""
+        """compass.h:145-150: step size back to the initial one, the loss's update(), loss of the current
+        parameters."""
         self.step_size = self.initial_step
-        self.loss_value = self.V(self.loss(self.full))
+        self.loss.update()
+        self.loss_value = self.V(self.loss(params=self.full))
 
     def is_converged(self):
         return bool(self.step_size < self.tolerance)
@@ -300,6 +443,7 @@ class Compass:
         V = self.V
         if self.is_converged():
             return V(0)
+        self.loss.update()                      # compass.h:102-103, before the probes
         param = self._params()
         s = self.step_size
         probes, in_box = [], []

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 10
+#define BBM_HIP_ABI_VERSION 11
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -358,6 +358,51 @@ int bbm_hip_loss_tree_f64(const bbm_hip_child_f64* tree, int ntree, const double
                           const double* ref_r, const double* ref_g, const double* ref_b,
                           int loss_kind, uint32_t component, uint32_t unit,
                           double* sums, void* workspace, size_t workspace_bytes, void* stream);
+
+/* bbm::batch (include/bbm/batch.h:27-92): the loss over a random subset of a sampled loss's samples, redrawn by each
+ * update().  Its indices come from bbm::rng<Size_t> (backbone/native/include/backbone/random.h:40-66: std::mt19937_64
+ * and std::uniform_int_distribution<Size_t> over [lower, upper], both ends included), restated here on the host so a
+ * batch holds the reference's indices for the same seed: batch(batchsize, loss, seed) is
+ *   bbm_hip_rng_init(&rng, seed, 0, loss.samples()) then, per update(), bbm_hip_rng_draw(&rng, index, batchsize)
+ * (batch.h:40-54; the upper end is the sample count itself, an index the sampled loss masks to 0, :65-66).
+ * Caller-owned state, host only. */
+typedef struct bbm_hip_rng
+{
+  uint64_t mt[312];
+  uint64_t pos;
+  uint64_t lower, upper;
+} bbm_hip_rng;
+int bbm_hip_rng_init(bbm_hip_rng* rng, uint64_t seed, uint64_t lower, uint64_t upper);
+int bbm_hip_rng_draw(bbm_hip_rng* rng, uint64_t* out, size_t n);     /* out: host memory */
+/* The default seed of bbm::rng (std::mt19937_64::default_seed) */
+#define BBM_HIP_RNG_DEFAULT_SEED 5489u
+
+/* A batch's samples, gathered densely in draw order: dst[k][j] = src[k][index[i]] over the i with index[i] < nsamples
+ * (a larger index is the reference's masked lane, which adds 0), for narrays (<= 16) device arrays of nsamples values
+ * -- e.g. the materialised pairs (in xyz, out xyz) and reference table (r, g, b) of a fit.  index: HOST memory (the
+ * drawn indices); src / dst: host arrays of device pointers, dst arrays with room for count values.  Any loss entry
+ * point then scores the batch (bbm_hip_loss_pairs / _tree / _tree_f64 on the first n = returned count pairs).
+ * Returns the number of samples gathered (>= 0) or an error code; returns after the gather has completed. */
+int bbm_hip_gather_samples(const uint64_t* index, size_t count, uint64_t nsamples, const float* const* src,
+                           float* const* dst, int narrays, void* stream);
+int bbm_hip_gather_samples_f64(const uint64_t* index, size_t count, uint64_t nsamples, const double* const* src,
+                               double* const* dst, int narrays, void* stream);
+
+/* RCCL for the loss reduction of a fit sharded over GPUs (one process per GPU): each rank scores every probe of a
+ * compass step on its shard (bbm_hip_loss* -> sums), then the nprobes double sums are all-reduced in place (RCCL over
+ * xGMI, ncclSum on ncclFloat64) and every rank takes the same compass decision (include/optimizer/compass.h:122-126).
+ * Rank 0 makes the unique id (bbm_hip_comm_unique_id) and hands its bytes to the other ranks by any means (MPI, a
+ * file, a torch.distributed broadcast); every rank then calls bbm_hip_comm_init on its own current HIP device.
+ * librccl is loaded on first use (BBM_HIP_ERR_UNSUPPORTED without it). */
+#define BBM_HIP_COMM_ID_BYTES 128
+typedef struct bbm_hip_comm bbm_hip_comm;
+int bbm_hip_comm_unique_id(uint8_t* id, size_t bytes);
+int bbm_hip_comm_init(const uint8_t* id, size_t bytes, int rank, int world, bbm_hip_comm** comm);
+int bbm_hip_comm_destroy(bbm_hip_comm* comm);
+int bbm_hip_comm_rank(const bbm_hip_comm* comm);
+int bbm_hip_comm_size(const bbm_hip_comm* comm);
+/* sums[0 .. n-1] (device doubles) <- their sum over all ranks, on `stream` */
+int bbm_hip_allreduce_sums(bbm_hip_comm* comm, double* sums, size_t n, void* stream);
 
 /* The EPD model's shadowing table G1[p][t] (100 x 1000 floats, row-major; the reference's
  * include/precomputed/holzschuchpacanowski/G1.h), built on the current device on first use by

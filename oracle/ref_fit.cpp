@@ -11,7 +11,10 @@
  *   * sampledlossfunction (include/bbm/sampledlossfunction.h:34-97) with each of the six sample
  *     losses (include/loss/cosine_weighted_l2.h, cosine_weighted_log.h), per sample and as the
  *     reference's own serial float total;
- *   * compass search steps (include/optimizer/compass.h:40-183) on that loss.
+ *   * compass search steps (include/optimizer/compass.h:40-183) on that loss;
+ *   * bbm::batch (include/bbm/batch.h:27-92) over that loss: the indices its bbm::rng<Size_t> draws and the
+ *     per-sample losses operator()(idx) returns (its whole-batch operator() reads an uninitialised loop index,
+ *     batch.h:78, and is not called).
  * The reference model of a fit is a second instance of the same Aggregate type (a synthetic
  * "measured" material from a published fit): MERL .binary data does not exist in this container.
  */
@@ -23,6 +26,7 @@
 #include "linearizer/spherical_linearizer.h"
 #include "linearizer/merl_linearizer.h"
 #include "optimizer/compass.h"
+#include "bbm/batch.h"
 
 namespace bbmref {
 
@@ -286,6 +290,29 @@ int compass_run(const float* init, const float* rp, int np, const lin_desc& d, i
   });
 }
 
+// bbm::batch(batchsize, lf, seed) over the sampled loss, then `updates` more update() calls: per_sample receives
+// operator()(idx) for idx in [0, batchsize) after construction and after every update ((updates + 1) x batchsize)
+template<typename M>
+int batch_run(const float* fp, const float* rp, int np, const lin_desc& d, int loss_kind, uint64_t seed,
+              size_t batchsize, int updates, float* per_sample)
+{
+  const M fitted = ops<M>::make(fp, np);
+  const M reference = ops<M>::make(rp, np);
+  return with_lin(d, [&](auto lin) {
+    return with_loss<decltype(lin)>(loss_kind, [&](auto err) {
+      using LF = bbm::sampledlossfunction<M, M, decltype(err), decltype(lin)>;
+      LF lf(fitted, reference, err, lin);
+      bbm::batch<LF> b(batchsize, lf, seed);
+      for(int u = 0; u <= updates; ++u)
+      {
+        if(u > 0) b.update();
+        for(size_t i = 0; i < batchsize; ++i) per_sample[size_t(u) * batchsize + i] = b(i);
+      }
+      return int(lf.samples());
+    });
+  });
+}
+
 struct fit_entry
 {
   const char* name;
@@ -293,9 +320,11 @@ struct fit_entry
   std::vector<uint32_t> (*select)(uint32_t);
   int (*loss)(const float*, const float*, int, const lin_desc&, int, float*, float*, int);
   int (*compass)(const float*, const float*, int, const lin_desc&, int, int, float*, float*, float*);
+  int (*batch)(const float*, const float*, int, const lin_desc&, int, uint64_t, size_t, int, float*);
 };
 
-#define BBMREF_FIT(X, KEY) fit_entry{ KEY, &param_attrs<agg<X>>, &param_select<agg<X>>, &loss<agg<X>>, &compass_run<agg<X>> }
+#define BBMREF_FIT(X, KEY) fit_entry{ KEY, &param_attrs<agg<X>>, &param_select<agg<X>>, &loss<agg<X>>, &compass_run<agg<X>>, \
+                                      &batch_run<agg<X>> }
 
 const std::vector<fit_entry>& fit_registry()
 {
@@ -365,6 +394,19 @@ const std::vector<std::pair<const char*, std::vector<uint32_t> (*)()>>& agg_attr
   };
   return r;
 }
+
+// A sampled loss whose idx-th sample "loss" is idx itself (exact in float below 2^24): wrapped in the reference's
+// bbm::batch, operator()(i) then returns the i-th index its bbm::rng<Size_t> drew (batch.h:64-70)
+struct echo_loss
+{
+  BBM_IMPORT_CONFIG( C );
+  Size_t n;
+  void update(void) {}
+  Size_t samples(void) const { return n; }
+  Value operator()(Size_t idx, Mask = true) const { return Value(idx); }
+  Value operator()(Mask = true) const { return 0; }
+};
+static_assert(bbm::concepts::sampledlossfunction<echo_loss>);
 
 } // namespace bbmref
 
@@ -465,6 +507,29 @@ int bbmref_compass(const char* name, const float* init, const float* reference, 
   auto e = find_fit(name); if(!e) return -1;
   if(kind == 1) return -2;
   return e->compass(init, reference, np, desc_of(kind, s_in, s_out, rng), loss_kind, steps, params_out, loss_out, loss0);
+}
+
+// the indices of bbm::batch<...>(batchsize, loss with nsamples samples, seed) after construction and after each of
+// `updates` update() calls: (updates + 1) x batchsize values in [0, nsamples] (nsamples < 2^24)
+int bbmref_batch_indices(uint64_t seed, uint64_t nsamples, size_t batchsize, int updates, uint64_t* out)
+{
+  if(nsamples >= (uint64_t(1) << 24)) return -2;
+  bbm::batch<echo_loss> b(batchsize, echo_loss{size_t(nsamples)}, seed);
+  for(int u = 0; u <= updates; ++u)
+  {
+    if(u > 0) b.update();
+    for(size_t i = 0; i < batchsize; ++i) out[size_t(u) * batchsize + i] = uint64_t(float(b(i)));
+  }
+  return 0;
+}
+
+int bbmref_batch_loss(const char* name, const float* fitted, const float* reference, int np,
+                      int kind, const uint64_t* s_in, const uint64_t* s_out, const float* rng, int loss_kind,
+                      uint64_t seed, size_t batchsize, int updates, float* per_sample)
+{
+  auto e = find_fit(name); if(!e) return -1;
+  if(kind == 1) return -2;
+  return e->batch(fitted, reference, np, desc_of(kind, s_in, s_out, rng), loss_kind, seed, batchsize, updates, per_sample);
 }
 
 } // extern "C"

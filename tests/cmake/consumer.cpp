@@ -9,9 +9,18 @@
 #include "bsdfmodel/lambertian.h"
 #include "bsdfmodel/ward.h"
 #include "bbm_hip/batch.h"
+#include "bbm_hip/fit.h"
+#include "bbm_hip/check.h"
+#include "linearizer/spherical_linearizer.h"
 
 #include <cstdio>
 #include <string>
+
+// the fitting and checkBsdf API compile in a consumer of the reference's CMake target: the GPU sampled loss and its
+// batch satisfy the reference's loss concepts (compass takes either)
+using consumer_model = bbm::aggregatemodel<bbm::lambertian<bbm::floatRGB>, bbm::cooktorrance<bbm::floatRGB>>;
+static_assert(bbm::concepts::sampledlossfunction<bbm::hip::sampledlossfunction<consumer_model>>);
+static_assert(bbm::concepts::sampledlossfunction<bbm::hip::batch<bbm::hip::sampledlossfunction<consumer_model>>>);
 
 #ifndef BBM_BACKBONE_HIP
 #error "the HIP backbone's backbone.h was not the one included"

@@ -51,6 +51,13 @@
 #include "loss/cosine_weighted_log.h"
 #include "ref_he.hpp"
 #include "bbm_hip/batch.h"
+#include "bbm_hip/fit.h"
+#include "bbm_hip/check.h"
+#include "bbm/sampledlossfunction.h"
+#include "bbm/batch.h"
+#include "linearizer/spherical_linearizer.h"
+#include "optimizer/compass.h"
+#include "core/spherical.h"
 
 #include <hip/hip_runtime_api.h>
 
@@ -608,6 +615,202 @@ static bool check_exact(const MODEL& model, size_t n, unsigned seed)
   return differ == 0;
 }
 
+
+// ------------------------------------------------------------------ fitting and checkBsdf through the C++ API
+
+// bbm::hip::sampledlossfunction / batch / compass (bbm_hip/fit.h) against the reference's own sampledlossfunction,
+// batch and compass (sampledlossfunction.h:34-97, batch.h:27-92, compass.h:40-183) on the same model type, linearizer
+// and sample loss: per-sample losses, the total, a compass trajectory step by step (parameters bit for bit, losses at
+// 1e-5), the reference's own bbm::compass driving the GPU loss, the batch's per-sample losses after every update, and a
+// one-rank RCCL communicator.  MODEL: any composition (single kernel, composed, nested), floatRGB or doubleRGB.
+template<typename MODEL, bool COMPASS = true>
+static bool check_fit(const char* what, const MODEL& init, const MODEL& reference, int steps, unsigned seed)
+{
+  using C = bbm::get_config<MODEL>;
+  using V = bbm::Value_t<C>;
+  using LIN = bbm::spherical_linearizer<C>;
+  using ERR = bbm::standardLog_error<C>;
+  const LIN lin(bbm::vec2d<bbm::Size_t<C>>(12, 8), bbm::vec2d<bbm::Size_t<C>>(10, 6));
+  const ERR err;
+  bool ok = true;
+  double worst = 0;
+  auto rel = [&](double g, double w) {
+    const double e = (w == 0) ? (g == 0 ? 0.0 : 1.0) : std::fabs(g - w) / std::fabs(w);
+    worst = std::max(worst, e);
+    return e <= 1e-5;
+  };
+  // per-sample and total
+  MODEL fr = init, fg = init;
+  bbm::sampledlossfunction<MODEL, MODEL, ERR, LIN> rf(fr, reference, err, lin);
+  bbm::hip::sampledlossfunction<MODEL> gf(fg, reference, err, lin);
+  static_assert(bbm::concepts::sampledlossfunction<bbm::hip::sampledlossfunction<MODEL>>);
+  const size_t n = rf.samples();
+  ok &= (gf.samples() == n);
+  double want = 0;
+  for(size_t i = 0; i < n; ++i) want += double(rf(i));
+  for(size_t i = 0; i < n; i += 97) ok &= rel(double(gf(i)), double(rf(i)));
+  ok &= (gf(n) == 0) && (gf(n + 5) == 0);
+  ok &= rel(double(gf()), want / double(n));
+  // compass: the batched GPU compass vs the reference's compass, step by step (not for a nested aggregate: the
+  // reference cannot reflect its parameters as one vector, util/reflection.h:247, so its compass cannot hold them)
+  int same = 0;
+  if constexpr (COMPASS)
+  {
+    MODEL a = init, b = init, c = init;
+    bbm::sampledlossfunction<MODEL, MODEL, ERR, LIN> ra(a, reference, err, lin);
+    bbm::hip::sampledlossfunction<MODEL> gb(b, reference, err, lin);
+    bbm::hip::sampledlossfunction<MODEL> gc(c, reference, err, lin);
+    auto pa = bbm::parameter_values(a), pb = bbm::parameter_values(b), pc = bbm::parameter_values(c);
+    bbm::compass oa(ra, pa, bbm::parameter_lower_bound(a), bbm::parameter_upper_bound(a));
+    bbm::hip::compass ob(gb, pb, bbm::parameter_lower_bound(b), bbm::parameter_upper_bound(b));
+    bbm::compass oc(gc, pc, bbm::parameter_lower_bound(c), bbm::parameter_upper_bound(c));   // reference compass, GPU loss
+    for(int t = 0; t < steps; ++t)
+    {
+      const V la = oa.step(), lb = ob.step(), lc = oc.step();
+      bool eq = true;
+      for(size_t k = 0; k < pa.size(); ++k) eq &= (V(pa[k]) == V(pb[k])) && (V(pa[k]) == V(pc[k]));
+      if(!eq) break;
+      ok &= rel(double(lb), double(la)) && (lb == lc);
+      ++same;
+    }
+    ok &= (same == steps);
+  }
+  // batch: the same indices, the same per-sample losses, after construction and after each update
+  {
+    bbm::batch<decltype(rf)> rb(200, rf, seed);
+    bbm::hip::batch<decltype(gf)> gbt(200, gf, seed);
+    static_assert(bbm::concepts::sampledlossfunction<decltype(gbt)>);
+    for(int u = 0; u < 3; ++u)
+    {
+      if(u) { rb.update(); gbt.update(); }
+      for(size_t i = 0; i < 200; i += 7) ok &= rel(double(gbt(i)), double(rb(i)));
+      double bw = 0;
+      for(size_t i = 0; i < 200; ++i) bw += double(rb(i));
+      ok &= rel(double(gbt()), bw / 200.0);
+    }
+  }
+  // a one-rank RCCL communicator: the all-reduced sums are the shard's own
+  {
+    bbm::hip::comm cm(bbm::hip::comm::unique_id(), 0, 1);
+    bbm::hip::sampledlossfunction<MODEL> gcm(fg, reference, err, lin, &cm);
+    ok &= (gcm() == gf());
+  }
+  std::printf("{\"check\": \"fit_api\", \"model\": \"%s\", \"samples\": %zu, \"compass_steps_identical\": %d, "
+              "\"max_rel_err\": %.3e, \"ok\": %s}\n", what, n, same, worst, ok ? "true" : "false");
+  return ok;
+}
+
+// checkBsdf.cpp:28-35 sampleSphere: theta = safe_acos(1 - 2 xi0), phi = 2 pi xi1, pdf = 1 / 4pi
+static bbm::vec3d<float> sample_sphere(float xi0, float xi1, bool hemisphere, float& pdf)
+{
+  using namespace bbm;
+  using Constants = bbm::constants<float>;
+  bbm::vec2d<float> coord;
+  spherical::theta(coord) = hemisphere ? bbm::safe_acos(xi0) : bbm::safe_acos(1.0 - 2.0 * xi0);
+  spherical::phi(coord) = xi1 * Constants::Pi(2);
+  pdf = hemisphere ? float(1.0 / Constants::Pi(2)) : float(1.0 / Constants::Pi(4));
+  return spherical::convert(coord);
+}
+
+static std::vector<float> draws_host(int test, uint64_t seed, int slot, int draw, size_t n)
+{
+  dev_buf a(n), b(n);
+  HIPCHECK(hipSuccess);
+  bbm::hip::check(bbm_hip_check_draws(test, seed, slot, draw, 0, n, a.p, b.p, nullptr));
+  HIPCHECK(hipDeviceSynchronize());
+  std::vector<float> x = download(a, n), y = download(b, n);
+  x.insert(x.end(), y.begin(), y.end());
+  return x;
+}
+
+// bbm::hip::check_* (bbm_hip/check.h) vs the reference model evaluating the same draws on the CPU: the reflectance
+// test's estimate (sphere sampling), the pdf integral, and the pdf test's counts and mismatch
+template<typename MODEL>
+static bool check_stats(const MODEL& model, size_t samples)
+{
+  using C = bbm::get_config<MODEL>;
+  using Vec3d = typename MODEL::Vec3d;
+  const bbm::hip::model_desc m = bbm::hip::describe(model);
+  const uint64_t seed = 4242;
+  bool ok = true;
+  double worst = 0;
+  auto rel = [&](double g, double w, double tol) {
+    const double e = std::fabs(g - w) / std::max(std::fabs(w), 1e-30);
+    worst = std::max(worst, e);
+    return e <= tol;
+  };
+  const float eps = bbm::constants<float>::Epsilon();
+  // reflectance, 3 theta_out, sphere sampling (checkBsdf.cpp:77-90)
+  {
+    const size_t nt = 3;
+    const auto r = bbm::hip::check_reflectance(m, samples, nt, false, seed);
+    for(size_t t = 0; t < nt; ++t)
+    {
+      const auto xi = draws_host(BBM_CHECK_REFLECTANCE, seed, int(t), 0, samples);
+      const Vec3d out(r.out[t][0], r.out[t][1], r.out[t][2]);
+      double acc[3] = {0, 0, 0};
+      for(size_t s = 0; s < samples; ++s)
+      {
+        float pdf;
+        const Vec3d d = sample_sphere(xi[s], xi[samples + s], false, pdf);
+        if(!(pdf > eps)) continue;
+        const auto f = model.eval(d, out) * bbm::vec::z(d) / pdf;
+        for(int c = 0; c < 3; ++c) acc[c] += double(f[c]);
+      }
+      for(int c = 0; c < 3; ++c) ok &= rel(double(r.estimate[t][size_t(c)]), double(float(acc[c] / double(samples))), 1e-5);
+    }
+  }
+  // pdf integral over the sphere for 4 trial directions (checkBsdf.cpp:291-313)
+  {
+    const size_t trials = 4;
+    const auto r = bbm::hip::check_pdf_int(m, samples, trials, false, seed);
+    for(size_t t = 0; t < trials; ++t)
+    {
+      const auto xi = draws_host(BBM_CHECK_PDFINT, seed, int(t), 0, samples);
+      const Vec3d dt(r.direction[t][0], r.direction[t][1], r.direction[t][2]);
+      double pr = 0, pi = 0;
+      for(size_t s = 0; s < samples; ++s)
+      {
+        float sp;
+        const Vec3d d = sample_sphere(xi[s], xi[samples + s], false, sp);
+        if(!(sp > eps)) continue;
+        pr += double(model.pdf(d, dt, bbm::bsdf_flag::All, bbm::unit_t::Radiance) / sp);
+        pi += double(model.pdf(d, dt, bbm::bsdf_flag::All, bbm::unit_t::Importance) / sp);
+      }
+      ok &= rel(double(r.integral[t][0]), double(float(pr / double(samples))), 1e-5);
+      ok &= rel(double(r.integral[t][1]), double(float(pi / double(samples))), 1e-5);
+    }
+  }
+  // pdf test (checkBsdf.cpp:231-255): negative pdfs and the sample / pdf mismatch, hemisphere out directions
+  {
+    const auto r = bbm::hip::check_pdf(m, samples, false, seed);
+    const auto xo = draws_host(BBM_CHECK_PDF, seed, 0, 0, samples);
+    for(int k = 0; k < 2; ++k)
+    {
+      const auto xs = draws_host(BBM_CHECK_PDF, seed, 0, 1 + k, samples);
+      const bbm::unit_t unit = k ? bbm::unit_t::Importance : bbm::unit_t::Radiance;
+      size_t neg = 0;
+      double mis = 0;
+      for(size_t s = 0; s < samples; ++s)
+      {
+        float po;
+        const Vec3d out = sample_sphere(xo[s], xo[samples + s], true, po);
+        const auto smp = model.sample(out, bbm::vec2d<float>(xs[s], xs[samples + s]), bbm::bsdf_flag::All, unit);
+        const float p = model.pdf(smp.direction, out, bbm::bsdf_flag::All, unit);
+        neg += (p < 0);
+        mis += double(std::fabs(smp.pdf - p));
+      }
+      ok &= (r.negative[size_t(k)] == neg);
+      // directions agree per lane within the parity bar, so |sample.pdf - pdf| sums agree to its scale
+      ok &= std::fabs(double(r.mismatch[size_t(k)]) - mis / double(samples)) <= 1e-4 * std::max(1.0, mis / double(samples));
+    }
+  }
+  std::printf("{\"check\": \"check_api\", \"model\": \"%s\", \"samples\": %zu, \"max_rel_err\": %.3e, \"ok\": %s}\n",
+              json_escape(label(model)).c_str(), samples, worst, ok ? "true" : "false");
+  (void)sizeof(C);
+  return ok;
+}
+
 int main()
 {
   using F = bbm::floatRGB;
@@ -701,6 +904,32 @@ int main()
     auto p = bbm::parameter_values(ct_d);
     p[3] = 0.1 + 1e-12; p[4] = 1.5 + 3e-12;
     ok &= check_model_f64(ct_d, n, seed++);
+  }
+  // the C++ fitting and checkBsdf API (bbm_hip/fit.h, bbm_hip/check.h) against the reference's own objects
+  {
+    using agg3 = bbm::aggregatemodel<bbm::lambertian<F>, bbm::cooktorrance<F>, bbm::ggx<F>>;
+    agg3 i3, r3;
+    { auto p = bbm::parameter_values(r3, bbm::bsdf_attr(0x1F)); for(auto& x : p) x = float(x) * 1.15f; }
+    ok &= check_fit("Aggregate<Lambertian,CookTorrance,GGX>", i3, r3, 12, seed++);
+    using nest = bbm::aggregatemodel<bbm::aggregatemodel<bbm::lambertian<F>, bbm::ward<F>>, bbm::ggx<F>>;
+    nest in_, rn;
+    {
+      auto p = bbm::parameter_values(static_cast<bbm::aggregatemodel<bbm::lambertian<F>, bbm::ward<F>>&>(rn), bbm::bsdf_attr(0x1F));
+      for(auto& x : p) x = float(x) * 0.9f;
+      auto q = bbm::parameter_values(static_cast<bbm::ggx<F>&>(rn), bbm::bsdf_attr(0x1F));
+      for(auto& x : q) x = float(x) * 1.2f;
+    }
+    ok &= check_fit<nest, false>("Aggregate<Aggregate<Lambertian,Ward>,GGX>", in_, rn, 0, seed++);
+    agg_ct ic, rc;
+    { auto p = bbm::parameter_values(rc, bbm::bsdf_attr(0x1F)); for(auto& x : p) x = float(x) * 1.1f; }
+    ok &= check_fit("Aggregate<Lambertian,CookTorrance>", ic, rc, 12, seed++);
+    using aggb_d = bbm::aggregatemodel<bbm::lambertian<D>, bbm::bagher<D>>;
+    aggb_d ib, rb;
+    { auto p = bbm::parameter_values(rb, bbm::bsdf_attr(0x1F)); for(auto& x : p) x = double(x) * 0.95; }
+    ok &= check_fit("Aggregate<Lambertian,Bagher> (doubleRGB)", ib, rb, 6, seed++);
+    ok &= check_stats(bbm::cooktorrance<F>(), 1 << 16);
+    ok &= check_stats(agg3(), 1 << 16);
+    ok &= check_stats(agg_bagher(), 1 << 16);
   }
   return ok ? 0 : 1;
 }

@@ -562,6 +562,37 @@ def ref_pair_losses(name, fitted, reference, din, dout, loss_kind, nthreads=8):
     return per
 
 
+def ref_batch_indices(seed, nsamples, batchsize, updates):
+    """The indices the reference's bbm::batch draws (bbm::rng<Size_t>, batch.h:40-54) after construction and after
+    each of `updates` update() calls -> (updates + 1, batchsize) uint64 (oracle/ref_fit.cpp: bbmref_batch_indices)."""
+    lib = ref()
+    out = np.zeros((updates + 1, batchsize), np.uint64)
+    rc = lib.bbmref_batch_indices(ctypes.c_uint64(seed), ctypes.c_uint64(nsamples), ctypes.c_size_t(batchsize),
+                                  ctypes.c_int(updates), _fp(out))
+    assert rc == 0, rc
+    return out
+
+
+def ref_batch_losses(name, fitted, reference, grid, loss_kind, seed, batchsize, updates):
+    """batch::operator()(idx) of the reference's bbm::batch over its sampledlossfunction on a spherical grid, for
+    idx in [0, batchsize) after construction and after each update() -> (updates + 1, batchsize) float32."""
+    lib = ref()
+    s_in, s_out, rng = _grid_desc(grid)
+    fitted = np.ascontiguousarray(fitted, np.float32)
+    reference = np.ascontiguousarray(reference, np.float32)
+    out = np.zeros((updates + 1, batchsize), np.float32)
+    rc = lib.bbmref_batch_loss(name.encode(), _fp(fitted), _fp(reference), fitted.size, 0, _fp(s_in), _fp(s_out),
+                               _fp(rng), loss_kind, ctypes.c_uint64(seed), ctypes.c_size_t(batchsize),
+                               ctypes.c_int(updates), _fp(out))
+    assert rc > 0, rc
+    return out
+
+
+def golden_batch():
+    with open(os.path.join(GOLDEN, "batch.json")) as f:
+        return json.load(f)
+
+
 def ref_merl_index(din, dout, h=(1, 90), d=(180, 90)):
     """The reference merl_linearizer's inverse map (direction pair -> index)."""
     lib = ref()
@@ -586,6 +617,9 @@ class RefTotalLoss:
         self.grid = grid
         self.loss_kind = loss_kind
         self.calls = 0
+
+    def update(self):
+        """concepts::lossfunction's update() (sampledlossfunction.h:52: nothing to do)."""
 
     def probe_losses(self, probes):
         self.calls += 1

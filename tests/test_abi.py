@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 10
+    assert lib.bbm_hip_abi_version() == 11
 
 
 def test_f64_registry(lib):

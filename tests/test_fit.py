@@ -86,6 +86,9 @@ class _OracleShardLoss:
         self.probe_losses = fit.SampledLoss.probe_losses.__get__(self)
         self.__call__ = fit.SampledLoss.__call__.__get__(self)
 
+    def update(self):
+        pass
+
     def local_sums(self, probes):
         s = [np.sum(ou.ref_pair_losses(self.fitted.name, p, self.reference, self.din, self.dout, self.loss_kind),
                     dtype=np.float64) for p in np.asarray(probes, np.float32)]
