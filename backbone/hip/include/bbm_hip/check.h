@@ -59,7 +59,8 @@ namespace bbm {
           d.slot_x = sx; d.slot_y = sy; d.slot_z = sz;
           if(tree)
           {
-            const child_tree<float> c(m.composed() ? m : basic_model_desc<float>{BBM_HIP_AGGREGATE, {}, {m}});
+            // (the child arrays point into m: built from m itself, never from a temporary copy)
+            const child_tree<float> c(m);
             const bbm_hip_child leaf{m.id, m.params.data(), int(m.params.size()), nullptr, 0};
             check(bbm_hip_check_tree(m.composed() ? c.root : &leaf, m.composed() ? c.count : 1, &d, dacc.data(),
                                      dcnt.data(), ws.data(), wsb, stream));
@@ -70,7 +71,7 @@ namespace bbm {
         }
         else
         {
-          const child_tree<double> c(m.composed() ? m : basic_model_desc<double>{BBM_HIP_AGGREGATE, {}, {m}});
+          const child_tree<double> c(m);
           const bbm_hip_child_f64 leaf{m.id, m.params.data(), int(m.params.size()), nullptr, 0};
           check(bbm_hip_check_tree_f64(m.composed() ? c.root : &leaf, m.composed() ? c.count : 1, &d, sx, sy, sz,
                                        dacc.data(), dcnt.data(), ws.data(), wsb, stream));

@@ -38,11 +38,16 @@ struct Aggregate
   static constexpr bool kHasGeo = has_geo<A>() && has_geo<B>();
   struct Geo { typename A::Geo a; typename B::Geo b; };
   __device__ __forceinline__ static Geo geometry(v3 in, v3 out) { return Geo{A::geometry(in, out), B::geometry(in, out)}; }
+  __device__ __forceinline__ void eval_geo_cached(Geo& g, uint32_t component, float* rgb) const
+  {
+    eval_geo<true>(g, component, rgb);
+  }
+  template<bool CACHE = false>
   __device__ __forceinline__ void eval_geo(Geo& g, uint32_t component, float* rgb) const
   {
     float ra[3], rb[3];
-    a.eval_geo(g.a, component, ra);
-    b.eval_geo(g.b, component, rb);
+    geo_eval<CACHE>(a, g.a, component, ra);
+    geo_eval<CACHE>(b, g.b, component, rb);
     rgb[0] = ra[0] + rb[0];
     rgb[1] = ra[1] + rb[1];
     rgb[2] = ra[2] + rb[2];

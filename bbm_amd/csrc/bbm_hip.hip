@@ -435,6 +435,7 @@ int check_dirs(const float* x, const float* y, const float* z, const char* what)
 __global__ __launch_bounds__(kBlock) void k_fill_dirs(uint64_t key, uint64_t offset, uint64_t n, int mode,
                                                        float* __restrict__ x, float* __restrict__ y, float* __restrict__ z)
 {
+  math_tables_init();
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
   {
@@ -455,6 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(LinDesc d, uint64_t begin,
                                                       float* __restrict__ iy, float* __restrict__ iz, float* __restrict__ ox,
                                                       float* __restrict__ oy, float* __restrict__ oz)
 {
+  math_tables_init();
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
   {
@@ -490,6 +492,7 @@ int to_desc(const bbm_hip_linearizer* lin, LinDesc& d)
 
 __global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums, int nblocks, int nprobes, double* sums)
 {
+  math_tables_init();
   __shared__ double part[kBlock];
   const int p = blockIdx.x;
   double t = 0.0;
@@ -507,6 +510,7 @@ __global__ __launch_bounds__(kBlock) void k_loss_final(const double* block_sums,
 // partials [slot][b][kCheckAcc] -> acc[slot][kCheckAcc]: one wave per slot, fixed order
 __global__ __launch_bounds__(64) void k_check_final(const double* partial, int nblocks, double* acc)
 {
+  math_tables_init();
   const int slot = blockIdx.x;
   double r[kCheckAcc];
 #pragma unroll
@@ -535,6 +539,7 @@ namespace {
 
 __global__ __launch_bounds__(kBlock) void k_draws(uint64_t key, uint64_t offset, uint64_t n, float* u0, float* u1)
 {
+  math_tables_init();
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
     uniform2(key, offset + i, u0[i], u1[i]);
@@ -542,6 +547,7 @@ __global__ __launch_bounds__(kBlock) void k_draws(uint64_t key, uint64_t offset,
 
 __global__ __launch_bounds__(kBlock) void k_trials(uint64_t base, int ntrials, int sphere, float* x, float* y, float* z)
 {
+  math_tables_init();
   const int t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= ntrials) return;
   float u0, u1;
@@ -553,6 +559,7 @@ __global__ __launch_bounds__(kBlock) void k_trials(uint64_t base, int ntrials, i
 __global__ __launch_bounds__(kBlock) void k_sphere_dirs(const float* u0, const float* u1, uint64_t n, int hemisphere,
                                                         float* x, float* y, float* z)
 {
+  math_tables_init();
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
   {
@@ -564,6 +571,7 @@ __global__ __launch_bounds__(kBlock) void k_sphere_dirs(const float* u0, const f
 // bbm_hip_libm_eval: the device's restated libm floats, elementwise
 __global__ __launch_bounds__(kBlock) void k_libm(int func, const float* a, const float* b, float* out, uint64_t n)
 {
+  math_tables_init();
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
   {

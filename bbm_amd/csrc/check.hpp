@@ -122,6 +122,7 @@ template<class Model> struct check_waves { static constexpr int value = BBM_HIP_
 template<class Model, int TEST>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(check_waves<Model>::value, 8))) void k_check(CheckArgs a)
 {
+  math_tables_init();
   __shared__ double part[kBlock / 64][kCheckAcc];
   const Model m(a.p.v);
   const int slot = blockIdx.y;

@@ -59,6 +59,7 @@ template<> __device__ __forceinline__ double eps_of<double>() { return 2.2204460
 template<class T>
 __global__ __launch_bounds__(kB) void k_fold3(const T* tr, const T* tg, const T* tb, T* r, T* g, T* b, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) { r[i] = tr[i] + r[i]; g[i] = tg[i] + g[i]; b[i] = tb[i] + b[i]; }
 }
 
@@ -67,6 +68,7 @@ template<class T>
 __global__ __launch_bounds__(kB) void k_lfold3(const T* tr, const T* tg, const T* tb, T* r, T* g, T* b, uint64_t n,
                                                int first)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n)
   {
     // the accumulation starts from Spectrum(0): 0 + e0 first (-0 becomes +0), then + e_k
@@ -80,12 +82,14 @@ __global__ __launch_bounds__(kB) void k_lfold3(const T* tr, const T* tg, const T
 template<class T>
 __global__ __launch_bounds__(kB) void k_inner_bsdf(const T* p, const T* w, const T* sum, T* ip, uint64_t n, int first)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) ip[i] = (first ? T(0) : ip[i]) + (w[i] * p[i]) / sum[i];
 }
 
 template<class T>
 __global__ __launch_bounds__(kB) void k_mask_sum(const T* ip, const T* sum, T* pdf, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) pdf[i] = (sum[i] > eps_of<T>()) ? ip[i] : T(0);
 }
 
@@ -93,6 +97,7 @@ __global__ __launch_bounds__(kB) void k_mask_sum(const T* ip, const T* sum, T* p
 template<class T>
 __global__ __launch_bounds__(kB) void k_weight(const T* r, const T* g, const T* b, T* w, T* sum, uint64_t n, int first)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n)
   {
     const T wk = ((T(0) + r[i]) + g[i]) + b[i];
@@ -105,6 +110,7 @@ __global__ __launch_bounds__(kB) void k_weight(const T* r, const T* g, const T* 
 template<class T>
 __global__ __launch_bounds__(kB) void k_inner(const T* p, const T* w, T* ip, uint64_t n, int first)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) ip[i] = (first ? T(0) : ip[i]) + p[i] * w[i];
 }
 
@@ -112,6 +118,7 @@ __global__ __launch_bounds__(kB) void k_inner(const T* p, const T* w, T* ip, uin
 template<class T>
 __global__ __launch_bounds__(kB) void k_mix(const T* ip, const T* sum, T* pdf, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) pdf[i] = (sum[i] > eps_of<T>()) ? ip[i] / sum[i] : T(0);
 }
 
@@ -121,6 +128,7 @@ template<class T>
 __global__ __launch_bounds__(kB) void k_select(const T* w, int nchild, const T* sum, const T* xi0, const uint8_t* mask,
                                                int8_t* chosen, T* xs, uint64_t n, int bsdf)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n)
   {
     // aggregatebsdf: mask &= (sum > eps) before the selection (aggregatebsdf.h:115)
@@ -142,12 +150,14 @@ __global__ __launch_bounds__(kB) void k_select(const T* w, int nchild, const T* 
 
 __global__ __launch_bounds__(kB) void k_child_mask(const int8_t* chosen, int k, uint8_t* m, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) m[i] = (chosen[i] == k) ? 1 : 0;
 }
 
 template<class T>
 __global__ __launch_bounds__(kB) void k_zero_sample(T* x, T* y, T* z, uint32_t* flag, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n) { x[i] = T(0); y[i] = T(0); z[i] = T(0); flag[i] = kFlagNone; }
 }
 
@@ -155,6 +165,7 @@ template<class T>
 __global__ __launch_bounds__(kB) void k_take(const int8_t* chosen, int k, const T* tx, const T* ty, const T* tz,
                                              const uint32_t* tf, T* x, T* y, T* z, uint32_t* flag, uint64_t n)
 {
+  math_tables_init();
   BBM_GRID_LOOP(i, n)
     if (chosen[i] == k) { x[i] = tx[i]; y[i] = ty[i]; z[i] = tz[i]; flag[i] = tf[i]; }
 }
@@ -594,6 +605,7 @@ __global__ __launch_bounds__(kB) void k_loss_terms(const T* r, const T* g, const
                                                    const T* rr, const T* rg, const T* rb, int kind, uint64_t n,
                                                    double* block_sums, int p, int nprobes)
 {
+  math_tables_init();
   __shared__ double part[kB / 64];
   double acc = 0.0;
   BBM_GRID_LOOP(i, n)
@@ -715,6 +727,7 @@ __global__ __launch_bounds__(kB) void k_tree_gen(TreeCheckDims dm, uint64_t k0ba
                                                  T* ax, T* ay, T* az, T* bx, T* by, T* bz, T* x0, T* x1, T* y0,
                                                  T* y1, T* aux)
 {
+  math_tables_init();
   const uint64_t lanes = dm.len * uint64_t(dm.nsl);
   BBM_GRID_LOOP(j, lanes)
   {
@@ -794,6 +807,7 @@ __global__ __launch_bounds__(kB) void k_tree_acc(TreeCheckDims dm, const T* ax, 
                                                  const T* a2z, const T* aux, int include_zero, double* partial,
                                                  unsigned long long* counts)
 {
+  math_tables_init();
   __shared__ double part[kB / 64][kCheckAcc];
   const int sl = blockIdx.y;                     // slot within the chunk
   const int slot = dm.s0 + sl;

@@ -41,6 +41,7 @@ __device__ __forceinline__ void st(double* p, uint64_t t, const double* v)
 template<class Model, int V, bool MASK, int W = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W, 8))) void k_eval_pdf_f64(EvalArgsF64 a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t nv = a.n / V;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W, 8))) 
 template<class Model, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_reflectance_f64(ReflArgsF64 a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
@@ -85,6 +87,7 @@ __global__ __launch_bounds__(kBlock) void k_reflectance_f64(ReflArgsF64 a)
 template<class Model, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_sample_f64(SampleArgsF64 a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
@@ -143,6 +146,7 @@ template<> struct host_params<EpdM>
 template<class Model>
 __global__ __launch_bounds__(128) void k_he_cdf_f64(ParamBlockF64 p, uint32_t component, double* __restrict__ cdf)
 {
+  math_tables_init();
   __shared__ double sm[90];
   const Model m(p.v);
   const int i = threadIdx.x;

@@ -584,6 +584,7 @@ struct He
 template<class Model>
 __global__ __launch_bounds__(128) void k_he_cdf(ParamBlock p, uint32_t component, float* __restrict__ cdf)
 {
+  math_tables_init();
   __shared__ float s[kHeBins];
   const Model m(p.v);
   const int i = threadIdx.x;

@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void k_epd_p2(const float* __restrict__ dq, co
                                                  const float* __restrict__ rj, const float* __restrict__ prow,
                                                  const float* __restrict__ norm, float* __restrict__ out)
 {
+  math_tables_init();
   const int row = blockIdx.y;
   const int j = blockIdx.x * 256 + threadIdx.x;    // 1 .. 998 carry a finite tan(theta)
   if (j < 1 || j >= kEpdCols) return;

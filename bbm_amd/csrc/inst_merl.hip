@@ -8,6 +8,7 @@ BBM_HIP_MERL_MODELS(BBM_HIP_INSTANTIATE)
 // merl.h:199-203, one entry per thread: three f64 reads (one per channel plane), one 16 B f32 write
 __global__ __launch_bounds__(256) void k_merl_table(const double* __restrict__ raw, float4* __restrict__ table)
 {
+  math_tables_init();
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= kMerlSize) return;
   const double r = fmax(0.0, raw[i] * 1.0 / 1500.0);

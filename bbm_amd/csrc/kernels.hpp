@@ -129,6 +129,16 @@ __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, floa
 // per SIMD (too few to hide the f64 / transcendental latencies).
 template<class Model> struct eval_waves { static constexpr int value = 1; };
 
+// Whether k_eval_pdf_v4 issues a thread's first quad of loads before the LDS table prologue and the model's
+// construction (their latencies then overlap; the loaded registers stay live across both).  Measured (ms, 100 M /
+// 10 M pairs, profiles/r05_ab_prefetch.txt): CookTorrance headline 0.727 -> 0.700, AshikhminShirley 0.0655 -> 0.0621;
+// Bagher, whose constructor holds ~40 registers of channel setup, 0.125 -> 0.131 -- off for it.
+#ifdef BBM_HIP_NO_PREFETCH
+template<class Model> struct eval_prefetch { static constexpr bool value = false; };   // A/B
+#else
+template<class Model> struct eval_prefetch { static constexpr bool value = true; };
+#endif
+
 // Grid cap of the eval kernels (0 = a full grid, one workgroup per 1024 pairs).  The model is constructed once per
 // thread from the kernarg parameters; where that constructor is expensive (the Student-T NDF's two tgamma and a pow
 // per thread) a capped grid-stride launch amortises it over several iterations.
@@ -138,19 +148,25 @@ template<class Model, int MODE, bool MASK, bool NT, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR __attribute__((amdgpu_waves_per_eu(eval_waves<Model>::value, 8)))
 void k_eval_pdf_v4(EvalArgs a)
 {
-  const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  for (uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x; t < n4; t += stride)
+  uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  // the first quad's loads go out before the table prologue and the model's construction, so their latencies hide
+  // under the loads' (most threads of a full grid run exactly one iteration; eval_prefetch)
+  float4 ix, iy, iz, ox, oy, oz;
+  uint32_t mk = 0x01010101u;
+  const auto load = [&](uint64_t q) {
+    ix = ld4<NT>(a.ix, q); iy = ld4<NT>(a.iy, q); iz = ld4<NT>(a.iz, q);
+    ox = ld4<NT>(a.ox, q); oy = ld4<NT>(a.oy, q); oz = ld4<NT>(a.oz, q);
+    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[q];
+  };
+  constexpr bool pf = eval_prefetch<Model>::value;
+  if (pf && t < n4) load(t);
+  math_tables_init();
+  const Model m(a.p.v);
+  for (bool first = true; t < n4; t += stride, first = false)
   {
-    const float4 ix = ld4<NT>(a.ix, t);
-    const float4 iy = ld4<NT>(a.iy, t);
-    const float4 iz = ld4<NT>(a.iz, t);
-    const float4 ox = ld4<NT>(a.ox, t);
-    const float4 oy = ld4<NT>(a.oy, t);
-    const float4 oz = ld4<NT>(a.oz, t);
-    uint32_t mk = 0x01010101u;
-    if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[t];
+    if (!pf || !first) load(t);
     const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
     const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
     float r[4], g[4], b[4], p[4];
@@ -183,6 +199,7 @@ void k_eval_pdf_v4(EvalArgs a)
 template<class Model, int MODE, bool MASK, bool NT>
 __global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v8(EvalArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -243,6 +260,7 @@ __global__ __launch_bounds__(kBlock) BBM_HIP_KERNEL_ATTR void k_eval_pdf_v8(Eval
 template<class Model, int MODE, bool MASK, bool NT>
 __global__ __launch_bounds__(kBlock) void k_eval_pdf_pipe(EvalArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
@@ -297,6 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_pdf_pipe(EvalArgs a)
 template<class Model, int MODE, bool MASK, bool EXACT = false>
 __global__ __launch_bounds__(kBlock) void k_eval_pdf_v1(EvalArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
@@ -356,6 +375,7 @@ template<class Model> constexpr int stage_words()
 template<class Model, int MODE, bool MASK>
 __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compact(EvalArgs a)
 {
+  math_tables_init();
   constexpr int kTile = 4 * kBlock;
   __shared__ float job[6][kTile];      // live pairs' in.xyz, out.xyz; rows 0..3 then hold rgb, pdf
   __shared__ int wave_total[kBlock / 64];
@@ -581,6 +601,7 @@ __device__ __forceinline__ void one_sample(const Model& m, const SampleArgs& a, 
 template<class Model, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_sample_v4(SampleArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
@@ -621,6 +642,7 @@ __global__ __launch_bounds__(kBlock) void k_sample_v4(SampleArgs a)
 template<class Model, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_sample_v1(SampleArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
@@ -745,6 +767,7 @@ struct ReflArgs
 template<class Model>
 __global__ __launch_bounds__(kBlock) void k_reflectance(ReflArgs a)
 {
+  math_tables_init();
   const Model m(a.p.v);
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride)
@@ -797,6 +820,7 @@ struct LossArgs
 template<class Model>
 __global__ __launch_bounds__(64) void k_loss_models(LossArgs a)
 {
+  math_tables_init();
   const int p = blockIdx.x * 64 + threadIdx.x;
   if (p >= a.nprobes) return;
   ParamBlock q;
@@ -847,6 +871,7 @@ template<class Model> struct loss_waves { static constexpr int value = BBM_HIP_L
 template<class Model>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_waves<Model>::value, 8))) void k_loss(LossArgs a)
 {
+  math_tables_init();
   static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
   __shared__ double part[kBlock / 64][kProbeBatch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -877,7 +902,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_wav
           if (p0 + j >= a.nprobes) break;           // uniform
           const Model& m = *reinterpret_cast<const Model*>(a.models + size_t(p0 + j) * kLossModelBytes);
           float rgb[3];
-          m.eval_geo(geo, a.component, rgb);
+          geo_eval<true>(m, geo, a.component, rgb);
           acc[j] += double(sample_loss(a.loss_kind, s, rgb));
         }
       }
@@ -918,7 +943,7 @@ template<class Model, bool G = has_geo<Model>()> struct LossGeo
 {
   typename Model::Geo g;
   __device__ __forceinline__ void init(v3 in, v3 out) { g = Model::geometry(in, out); }
-  __device__ __forceinline__ void eval(const Model& m, uint32_t component, float* rgb) { m.eval_geo(g, component, rgb); }
+  __device__ __forceinline__ void eval(const Model& m, uint32_t component, float* rgb) { geo_eval<true>(m, g, component, rgb); }
 };
 template<class Model> struct LossGeo<Model, false>
 {
@@ -967,6 +992,7 @@ template<class Model> struct loss_pair_waves { static constexpr int value = BBM_
 template<class Model>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(loss_pair_waves<Model>::value, 8))) void k_loss_pairs(LossArgs a)
 {
+  math_tables_init();
   static_assert(sizeof(Model) <= kLossModelBytes, "model does not fit its loss workspace slot");
   extern __shared__ double part[];                       // [kBlock / 64][nprobes] (+ the models, BBM_HIP_LOSS_MODEL 2)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -66,6 +66,15 @@ template<class M> struct exact_sample { using type = M; };
 template<class M> using exact_sample_t = typename exact_sample<M>::type;
 template<class M> constexpr bool has_exact_sample() { return !__is_same(exact_sample_t<M>, M); }
 
+// eval at a prepared pair (has_geo models): CACHE = true where the model can keep per-pair terms across the parameter
+// vectors evaluated at the pair (the fitting loss's probes: Bagher's NDF term)
+template<bool CACHE, class Model, class G>
+__device__ __forceinline__ void geo_eval(const Model& m, G& g, uint32_t component, float* rgb)
+{
+  if constexpr (CACHE && requires { m.eval_geo_cached(g, component, rgb); }) m.eval_geo_cached(g, component, rgb);
+  else m.eval_geo(g, component, rgb);
+}
+
 template<int MODE, bool EXACT, class Model>
 __device__ __forceinline__ void model_eval_pdf(const Model& m, v3 in, v3 out, uint32_t comp, float* rgb, float& pdf)
 {
@@ -258,12 +267,32 @@ __device__ __constant__ const uint64_t kExpfTab[32] = {
     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
-// kExpfTab[j] for a per-lane j in [0, 32).  Default: a 64-bit gather from the constant table (an L1/L2 hit, but
-// a dependent memory access queued behind the kernel's streaming loads).  -DBBM_HIP_EXPF_BPERM: every lane holds
-// entry (lane & 31) in two VGPRs (one load per wave, loop-invariant) and the lookup is two ds_bpermute_b32 --
-// cross-lane moves through the LDS crossbar, no memory access.
+// The tables of the glibc restatements below (expf's 2^(j/32), logf's and powf's (1/c, log c)) are read per lane with a
+// data-dependent index.  From the constant segment each lookup is a divergent 8-16 B gather through the vector memory
+// pipeline, queued behind the kernel's streaming loads; so every kernel of the library copies them into LDS first
+// (math_tables_init()) and looks them up with ds_read_b64 -- conflict-free, as each table spans the 64 banks once.
+// Every wave writes the whole table itself (lanes 0..31; all waves of a workgroup write the same values to the same
+// addresses) and reads it back in program order: no workgroup barrier delays the first streaming loads (with wave 0
+// filling the table for all behind one s_barrier, the memory-bound headline kernel lost 1.7 %; with a private copy per
+// wave, indexed by the wave id, Bagher and the He family lost 10-40 % to the extra addressing).  Measured against the
+// constant-segment gathers (profiles/r05_ab_lds_tables.txt, ms per 10 M pairs): the powf / logf lobes
+// (AshikhminShirley, Phong, Lafortune and their Ngan / Low forms) -5 to -12 %, PhongWalter -3.5 %, HeHolzschuch -4 %,
+// the Beckmann models -1 to -2 %; the models that read no table pay the prologue: GGX / GGXHeitz / LowSmooth +3-4 %.
+// -DBBM_HIP_EXPF_BPERM: every lane holds entry (lane & 31) in two VGPRs and the lookup is two ds_bpermute_b32.
+// -DBBM_HIP_CONST_TABLES (A/B): the constant-segment gathers.
+#ifndef BBM_HIP_CONST_TABLES
+static __shared__ uint64_t g_lds_exptab[32];
+static __shared__ double g_lds_logftab[16][2];
+static __shared__ double g_lds_log2tab[16][2];
+#endif
+// LDS = false: the constant-segment table (for code that runs out of line, where a gather is cheaper than keeping the
+// kernel's LDS copy reachable -- Bagher's shadowing tail)
+template<bool LDS = true>
 __device__ __forceinline__ uint64_t expf_tab(uint32_t j)
 {
+#ifndef BBM_HIP_CONST_TABLES
+  if constexpr (LDS) return g_lds_exptab[j];
+#endif
 #ifdef BBM_HIP_EXPF_BPERM
   const uint64_t mine = kExpfTab[__lane_id() & 31u];
   const int lo = __builtin_amdgcn_ds_bpermute(int(j << 2), int(uint32_t(mine)));
@@ -274,6 +303,7 @@ __device__ __forceinline__ uint64_t expf_tab(uint32_t j)
 #endif
 }
 
+template<bool LDS = true>
 __device__ __forceinline__ float expf_glibc(float x)
 {
   constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
@@ -289,7 +319,7 @@ __device__ __forceinline__ float expf_glibc(float x)
   // timing probe only (tools/build_variant.sh): the table gather replaced by arithmetic of the same shape (wrong values)
   const double s = __builtin_bit_cast(double, (0x3fef000000000000ull | ((ki & 31u) << 40)) + (ki << 47));
 #else
-  const double s = __builtin_bit_cast(double, expf_tab(ki & 31u) + (ki << 47));   // 2^(k/N)
+  const double s = __builtin_bit_cast(double, expf_tab<LDS>(ki & 31u) + (ki << 47));   // 2^(k/N)
 #endif
   const double z = __builtin_fma(kC0, r, kC1);
   const double r2 = r * r;
@@ -302,7 +332,7 @@ __device__ __forceinline__ float expf_glibc(float x)
 // the exponential of the eval kernels' Gaussian-like lobes (Ward, EPD; -DBBM_HIP_LOBES_EXP_DN: the 1.4-ulp
 // expf_dn, A/B).  Measured against expf_dn (tools/gpu_r03_e.sh, ms per 10 M pairs / bit-exact lanes): Ward
 // 0.060 -> 0.060 ms, 97.0 -> 99.7 %; EPD 0.270 -> 0.285 ms, 80.1 -> 83.5 %
-__device__ __forceinline__ float expf_glibc_neg(float x);
+template<bool LDS = true> __device__ __forceinline__ float expf_glibc_neg(float x);
 __device__ __forceinline__ float expf_lobe(float x)
 {
 #ifdef BBM_HIP_LOBES_EXP_DN
@@ -313,6 +343,7 @@ __device__ __forceinline__ float expf_lobe(float x)
 }
 
 // the same for x <= 0 or NaN (an exponent that is minus a square or a quotient of squares): no overflow select
+template<bool LDS>
 __device__ __forceinline__ float expf_glibc_neg(float x)
 {
   constexpr double kInvLn2N = 0x1.71547652b82fep+0 * 32;
@@ -324,7 +355,7 @@ __device__ __forceinline__ float expf_glibc_neg(float x)
   const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
   const double kd = kb - kShift;
   const double r = __builtin_fma(kInvLn2N, xd, -kd);
-  const double s = __builtin_bit_cast(double, expf_tab(ki & 31u) + (ki << 47));
+  const double s = __builtin_bit_cast(double, expf_tab<LDS>(ki & 31u) + (ki << 47));
   const double z = __builtin_fma(kC0, r, kC1);
   const double r2 = r * r;
   double y = __builtin_fma(kC2, r, 1.0);
@@ -360,6 +391,40 @@ __device__ __constant__ const double kPowfLog2Tab[16][2] = {    // {1/c, log2 c}
     {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
     {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2}, {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}};
 
+template<bool LDS = true>
+__device__ __forceinline__ double powf_log2tab(uint32_t i, int c)
+{
+#ifndef BBM_HIP_CONST_TABLES
+  if constexpr (LDS) return g_lds_log2tab[i][c];
+#endif
+  return kPowfLog2Tab[i][c];
+}
+template<bool LDS = true>
+__device__ __forceinline__ double logf_tab(uint32_t i, int c)
+{
+#ifndef BBM_HIP_CONST_TABLES
+  if constexpr (LDS) return g_lds_logftab[i][c];
+#endif
+  return kLogfTab[i][c];
+}
+// Every kernel's first statement (tests/test_kernel_prologue.py checks that every kernel of the library starts with
+// it): lanes 0..31 of every wave fill the tables; the wave's later reads of them follow in program order (a
+// wavefront-scope fence keeps the compiler from moving them above the stores)
+__device__ __forceinline__ void math_tables_init()
+{
+#ifndef BBM_HIP_CONST_TABLES
+  const unsigned t = threadIdx.x & 63u;
+  if (t < 32)
+  {
+    g_lds_exptab[t] = kExpfTab[t];
+    g_lds_logftab[t >> 1][t & 1] = kLogfTab[t >> 1][t & 1];
+    g_lds_log2tab[t >> 1][t & 1] = kPowfLog2Tab[t >> 1][t & 1];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 // x = 2^k z with z in [0x3f330000, 2 x 0x3f330000): the bits of z, k, and the table row (subnormal x normalised)
 __device__ __forceinline__ uint32_t glibcf_reduce(float x, uint32_t& i, int& k)
 {
@@ -371,13 +436,14 @@ __device__ __forceinline__ uint32_t glibcf_reduce(float x, uint32_t& i, int& k)
   return ix - (tmp & 0xff800000u);
 }
 
+template<bool LDS = true>
 __device__ __forceinline__ float logf_glibc(float x)
 {
   uint32_t i;
   int k;
   const double z = double(__uint_as_float(glibcf_reduce(x, i, k)));
-  const double r = __builtin_fma(z, kLogfTab[i][0], -1.0);
-  const double y0 = __builtin_fma(double(k), 0x1.62e42fefa39efp-1, kLogfTab[i][1]);
+  const double r = __builtin_fma(z, logf_tab<LDS>(i, 0), -1.0);
+  const double y0 = __builtin_fma(double(k), 0x1.62e42fefa39efp-1, logf_tab<LDS>(i, 1));
   const double r2 = r * r;
   double y = __builtin_fma(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
   y = __builtin_fma(-0x1.00ea348b88334p-2, r2, y);
@@ -389,13 +455,14 @@ __device__ __forceinline__ float logf_glibc(float x)
 }
 
 // powf for x >= 0 (or NaN), any y (the reference's uses: a distance or a sum of squares to a parameter power)
+template<bool LDS = true>
 __device__ __forceinline__ float powf_glibc(float x, float y)
 {
   uint32_t i;
   int k;
   const double z = double(__uint_as_float(glibcf_reduce(x, i, k)));
-  const double r = __builtin_fma(z, kPowfLog2Tab[i][0], -1.0);
-  const double y0 = kPowfLog2Tab[i][1] + double(k);
+  const double r = __builtin_fma(z, powf_log2tab<LDS>(i, 0), -1.0);
+  const double y0 = powf_log2tab<LDS>(i, 1) + double(k);
   const double r2 = r * r;
   double q0 = __builtin_fma(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
   const double p = __builtin_fma(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
@@ -408,7 +475,7 @@ __device__ __forceinline__ float powf_glibc(float x, float y)
   const double kb = ylogx + kShift;
   const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
   const double rr = ylogx - (kb - kShift);
-  const double s = __builtin_bit_cast(double, expf_tab(uint32_t(ki) & 31u) + (ki << 47));
+  const double s = __builtin_bit_cast(double, expf_tab<LDS>(uint32_t(ki) & 31u) + (ki << 47));
   const double zz = __builtin_fma(0x1.c6af84b912394p-5, rr, 0x1.ebfce50fac4f3p-3);
   double e = __builtin_fma(0x1.62e42ff0c52d6p-1, rr, 1.0);
   e = __builtin_fma(zz, rr * rr, e);
@@ -420,6 +487,39 @@ __device__ __forceinline__ float powf_glibc(float x, float y)
   res = (x == __builtin_inff()) ? ((y < 0.0f) ? 0.0f : __builtin_inff()) : res;
   res = (x != x || y != y || x < 0.0f) ? __builtin_nanf("") : res;
   return (y == 0.0f || x == 1.0f) ? 1.0f : res;
+}
+
+// powf_glibc for a finite normal x > 0 and a finite y: the same steps without the special-operand selects and the
+// subnormal normalisation (pow(1, y) and pow(x, 0) come out as exactly 1 from the table row {1, 0} and r = 0), for the
+// sites whose base is provably a positive normal float (Bagher's t = alpha + tan^2 / alpha, alpha >= its lower bound)
+template<bool LDS = true>
+__device__ __forceinline__ float powf_glibc_pos(float x, float y)
+{
+  const uint32_t ix = __float_as_uint(x);
+  const uint32_t tmp = ix - 0x3f330000u;
+  const uint32_t i = (tmp >> 19) & 15u;
+  const int k = int32_t(tmp) >> 23;
+  const double z = double(__uint_as_float(ix - (tmp & 0xff800000u)));
+  const double r = __builtin_fma(z, powf_log2tab<LDS>(i, 0), -1.0);
+  const double y0 = powf_log2tab<LDS>(i, 1) + double(k);
+  const double r2 = r * r;
+  const double q0 = __builtin_fma(0x1.27616c9496e0bp-2, r, -0x1.71969a075c67ap-2);
+  const double p = __builtin_fma(0x1.ec70a6ca7baddp-2, r, -0x1.7154748bef6c8p-1);
+  const double r4 = r2 * r2;
+  double q = __builtin_fma(0x1.71547652ab82bp+0, r, y0);
+  q = __builtin_fma(p, r2, q);
+  const double ylogx = double(y) * __builtin_fma(q0, r4, q);
+  constexpr double kShift = 0x1.8p+52 / 32;
+  const double kb = ylogx + kShift;
+  const uint64_t ki = uint64_t(__builtin_bit_cast(int64_t, kb));
+  const double rr = ylogx - (kb - kShift);
+  const double s = __builtin_bit_cast(double, expf_tab<LDS>(uint32_t(ki) & 31u) + (ki << 47));
+  const double zz = __builtin_fma(0x1.c6af84b912394p-5, rr, 0x1.ebfce50fac4f3p-3);
+  double e = __builtin_fma(0x1.62e42ff0c52d6p-1, rr, 1.0);
+  e = __builtin_fma(zz, rr * rr, e);
+  float res = float(e * s);
+  res = (ylogx > 0x1.fffffffd1d571p+6) ? __builtin_inff() : res;
+  return (ylogx <= -150.0) ? 0.0f : res;
 }
 
 // glibc 2.35's erff / erfcf (sysdeps/ieee754/flt-32/s_erff.c: Sun fdlibm's rational approximations in float
@@ -704,7 +804,7 @@ __device__ __forceinline__ float powf_fast(float x, float y)
 // bbm::pow of two floats where the result is a model's value factor (Phong / Lafortune / Ashikhmin-Shirley lobes,
 // the Phong NDF): glibc's powf to its last bit by default; -DBBM_HIP_POWF_FAST (A/B): the ~1e-6 powf_fast
 __device__ __forceinline__ float powf_fast(float x, float y);
-__device__ __forceinline__ float powf_glibc(float x, float y);
+template<bool LDS> __device__ __forceinline__ float powf_glibc(float x, float y);
 __device__ __forceinline__ float powf_ref(float x, float y)
 {
 #ifdef BBM_HIP_POWF_FAST

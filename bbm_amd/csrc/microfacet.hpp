@@ -8,6 +8,11 @@
 #pragma once
 #include "math.hpp"
 
+// where the Beckmann NDF's expf reads its table (math.hpp expf_tab): 1 = the kernel's LDS copy, 0 = the constant segment
+#ifndef BBM_HIP_BECKMANN_TABLE_LDS
+#define BBM_HIP_BECKMANN_TABLE_LDS 1
+#endif
+
 namespace bbmhip {
 
 // ------------------------------------------------------------------------------------- NDFs
@@ -46,7 +51,7 @@ struct Beckmann
 #elif defined(BBM_HIP_BECKMANN_EXP_RN)
     float D = div_nr(expf_rn(div_nr(-sn, c2)), au * av * c2 * c2);      // A/B: correctly rounded
 #else
-    float D = div_sub<EXACT>(expf_glibc_neg(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit (x <= 0)
+    float D = div_sub<EXACT>(expf_glibc_neg<BBM_HIP_BECKMANN_TABLE_LDS != 0>(div_nr(-sn, c2)), au * av * c2 * c2);   // glibc's expf, to its last bit (x <= 0)
 #endif
     if (Normalize) D *= kInvPiF;
     return (h.z > 0) ? D : 0.0f;

@@ -22,6 +22,7 @@ template<class B> struct compact_eval<Aggregate<Lambertian, B>> { static constex
 template<class B> struct eval_waves<Aggregate<Lambertian, B>> { static constexpr int value = eval_waves<B>::value; };
 template<class B> struct loss_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_waves<B>::value; };
 template<class B> struct eval_grid_cap<Aggregate<Lambertian, B>> { static constexpr uint64_t value = eval_grid_cap<B>::value; };
+template<class B> struct eval_prefetch<Aggregate<Lambertian, B>> { static constexpr bool value = eval_prefetch<B>::value; };
 template<class FRES, bool ERRATA, bool WESTIN, int TAYLOR, bool ADAPTIVE, int APPROX, bool SCALED>
 struct loss_waves<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>> { static constexpr int value = 1; };
 template<class B> struct loss_pair_waves<Aggregate<Lambertian, B>> { static constexpr int value = loss_pair_waves<B>::value; };
@@ -47,6 +48,10 @@ template<> struct loss_pair_waves<Bagher> { static constexpr int value = BBM_HIP
 #define BBM_HIP_BAGHER_WAVES 3
 #endif
 template<> struct eval_waves<Bagher> { static constexpr int value = BBM_HIP_BAGHER_WAVES; };
+template<> struct eval_prefetch<Bagher> { static constexpr bool value = false; };
+#ifdef BBM_HIP_BAGHER_COMPACT
+template<> struct compact_eval<Bagher> { static constexpr bool value = true; };   // A/B
+#endif
 #ifdef BBM_HIP_MERL_WAVES
 template<> struct eval_waves<Merl> { static constexpr int value = BBM_HIP_MERL_WAVES; };   // A/B
 #endif

@@ -119,7 +119,9 @@ struct Bagher
   // (the loss kernel spilled 124 VGPRs instead of 69) although at the default theta0 = pi/2 no lane takes them
   __device__ __attribute__((noinline, pure)) static float g1_tail(float d, float c, float k, float Lambda)
   {
-    return 1.0f + Lambda * (1.0f - expf_glibc(c * powf_glibc(d, k)));
+    // the constant-segment tables here: this out-of-line tail reading the kernel's LDS copies cost the fitting loss
+    // kernel (8 waves per SIMD, spilling) ~13 % per compass step
+    return 1.0f + Lambda * (1.0f - expf_glibc<false>(c * powf_glibc<false>(d, k)));
   }
   // the same for an upper-hemisphere direction with squared chord q: lanes below the conservative threshold have
   // theta <= theta0 and G1 = 1; the others evaluate G1 exactly as above, on a branch (the shadowing term's double
@@ -141,6 +143,12 @@ struct Bagher
     float outh, tan2, q_in, q_out, th_in, th_out, cosF, zz;
     double dnorm, x5;
     bool sdirs, gmask;
+    // the fitting loss's per-pair cache of the NDF term P22 = e^-t / t^p per channel, with the (alpha, p) it was
+    // computed for, filled by the pair's first probe: a compass step's probes each move one parameter off the current
+    // point, so all but the probes on channel j's alpha or p reuse it (eval_geo<..., true>).  Measured on config 5, ms
+    // per compass step (profiles/r05_ab_fit_p22_cache.txt): no cache 0.675, refilled on every miss 0.438, filled
+    // once 0.425; the round-4 fast D 0.411
+    float ca[3], cp[3], cP22[3];
   };
 
   __device__ __forceinline__ static Geo geometry(v3 in, v3 out)
@@ -164,39 +172,70 @@ struct Bagher
     const double x = double(1.0f - g.cosF);
     g.x5 = (x * x) * (x * x) * x;
     g.zz = in.z * out.z;
+    for (int j = 0; j < 3; ++j) g.ca[j] = g.cp[j] = g.cP22[j] = __builtin_nanf("");   // no cached term yet
     return g;
   }
 
-  // eval (Specular component) at a prepared pair; EXACT (exact mode): the NDF's power and exponential by glibc's own
-  // powf / expf, so D is the reference's float -- Bagher and Aggregate(Lambertian, Bagher) then bit-identical on
-  // nearly every lane, for +68 % kernel time (profiles/r04_ab_bagher_exact_d.txt)
-  template<bool EXACT = false>
+  // eval (Specular component) at a prepared pair.  The NDF's power and exponential are glibc's own powf / expf (round
+  // 5: by default; round 4 only in exact mode), so D is the reference's float -- Bagher and Aggregate(Lambertian,
+  // Bagher) bit-identical on nearly every lane (the rest below 1e-30); +13 % kernel time against round 4's fast D
+  // (0.108 -> 0.122 ms per 10 M pairs on one box, profiles/r05_ab_bagher_exact_d.txt; round 4's exact form: +68 %):
+  // the LDS tables, the positive-normal powf, and the three channels' D chains in one branch-free block.  EXACT (exact
+  // mode) adds the subnormal quotients of eval_scale.
+  // EXACT_D = false (A/B builds with -DBBM_HIP_BAGHER_FAST_D): the round-4 D by powf_fast / expf_dn (~1e-6 relative).
+  // CACHE (the fitting loss kernels): reuse the pair's P22 of channel j where the probe's (alpha_j, p_j) equal the
+  // ones it was computed for -- the same float, computed once instead of once per probe.
+#ifdef BBM_HIP_BAGHER_FAST_D
+  static constexpr bool kExactD = false;
+#else
+  static constexpr bool kExactD = true;
+#endif
+  template<bool EXACT = false, bool EXACT_D = kExactD, bool CACHE = false>
   __device__ __forceinline__ void eval_geo(Geo& g, uint32_t component, float* rgb) const
   {
     const bool active = (component & kFlagSpecular) && g.sdirs;
+    // the three channels' NDF terms first, in one branch-free block (eval): their dependent f64 and LDS-table chains
+    // interleave there, where the shadowing branches below would otherwise serialise them channel by channel
+    float P22[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+    {
+      bool hit = false;
+      if constexpr (CACHE) hit = (alpha[j] == g.ca[j]) && (p[j] == g.cp[j]);
+      if (hit) P22[j] = g.cP22[j];
+      else
+      {
+        // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154): exp(-t) / t^p with t = alpha + tan^2 / alpha
+        const float t = alpha[j] + div_nr(g.tan2, alpha[j]);
+        if constexpr (EXACT || EXACT_D)
+        {
+          // glibc's powf and expf restated (math.hpp), so D is the reference's float.  t >= alpha >= the parameter's
+          // lower bound (Epsilon, bsdf_attribute.h:77) is a normal float (or +inf where tan^2 is, which gives the
+          // reference's P22 = 0 here as well), so the power takes glibc's path for normal positive bases
+          const float den = powf_glibc_pos(t, p[j]);
+          P22[j] = (den > kEpsF) ? div_nr(expf_glibc_neg(-t), den) : 0.0f;
+        }
+        else
+        {
+          const float den = powf_fast(t, p[j]);
+          P22[j] = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
+        }
+        if constexpr (CACHE)
+        if (g.ca[j] != g.ca[j])   // filled by the pair's first probe only (see Geo)
+        {
+          g.ca[j] = alpha[j];
+          g.cp[j] = p[j];
+          g.cP22[j] = P22[j];
+        }
+      }
+    }
     // in.z, out.z > 0 on every lane whose result is used: theta_of only where a channel may need it
     if (g.q_in > qc_min && g.th_in < 0.0f) g.th_in = theta_of(g.in);
     if (g.q_out > qc_min && g.th_out < 0.0f) g.th_out = theta_of(g.out);
 #pragma unroll
     for (int j = 0; j < 3; ++j)
     {
-      // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154)
-      const float t = alpha[j] + div_nr(g.tan2, alpha[j]);
-      // exp(-t) / t^p: powf_fast (~1e-6) instead of the 173-instruction library powf.  Next to that factor the
-      // glibc-exact expf buys nothing (bit-exact lanes 68.9 -> 69.7 %) and cost 12 % (0.162 -> 0.183 ms per
-      // 10 M pairs, tools/gpu_r03_e.sh): expf_dn here
-      float P22;
-      if constexpr (EXACT)
-      {
-        const float den = powf_glibc(t, p[j]);
-        P22 = (den > kEpsF) ? div_nr(expf_glibc_neg(-t), den) : 0.0f;
-      }
-      else
-      {
-        const float den = powf_fast(t, p[j]);
-        P22 = (den > kEpsF) ? div_nr(expf_dn(-t), den) : 0.0f;
-      }
-      const float Dj = ((g.h.z > 0) ? f_div_d(double(P22), g.dnorm) : 0.0f) * K[j];
+      const float Dj = ((g.h.z > 0) ? f_div_d(double(P22[j]), g.dnorm) : 0.0f) * K[j];
       const float Gj = g.gmask ? G1q(j, g.q_in, g.th_in) * G1q(j, g.q_out, g.th_out) : 0.0f;
       // fresnel::bagher (bagher.h:46-49): schlick(F0) rounded to float, minus F1 cos
       const float S = float(double(F0[j]) + double(1.0f - F0[j]) * g.x5);
@@ -206,13 +245,21 @@ struct Bagher
     }
   }
 
+  __device__ __forceinline__ void eval_geo_cached(Geo& g, uint32_t component, float* rgb) const
+  {
+#ifdef BBM_HIP_BAGHER_NO_P22_CACHE
+    eval_geo<false, kExactD, false>(g, component, rgb);   // A/B
+#else
+    eval_geo<false, kExactD, true>(g, component, rgb);
+#endif
+  }
+
   static constexpr bool kHasExact = true;
   template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
   {
     Geo g = geometry(in, out);
-    if (MODE & kModeEval) eval_geo<EXACT>(g, component, rgb);
-    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
+    // the pdf first: straight-line code that schedules with the geometry and eval_geo's NDF block
     if (MODE & kModePdf)
     {
       const bool active = (component & kFlagSpecular) && g.sdirs;
@@ -221,6 +268,8 @@ struct Bagher
       pdf = active ? pp : 0.0f;
     }
     else pdf = 0.0f;
+    if (MODE & kModeEval) eval_geo<EXACT>(g, component, rgb);
+    else rgb[0] = rgb[1] = rgb[2] = 0.0f;
   }
 
   // microfacet.h:182-196 with fresnel::bagher at cos = z(out), x albedo (scaledmodel.h:64-67)

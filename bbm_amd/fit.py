@@ -134,6 +134,15 @@ class SampledLoss:
             self.pairs = tuple(pairs)
             self.n = self.total = int(self.pairs[0].shape[1])
             self.begin = 0
+            if dist is not None and dist.get_world_size() > 1:
+                # every rank holds its own pairs: the grid is their concatenation in rank order (total = the sum of
+                # the counts, this rank's samples start after the lower ranks'), so the losses are means over all
+                counts = _torch().zeros(dist.get_world_size(), dtype=_torch().int64, device=self.pairs[0].device)
+                counts[dist.get_rank()] = self.n
+                dist.all_reduce(counts)
+                counts = counts.cpu().tolist()
+                self.total = int(sum(counts))
+                self.begin = int(sum(counts[:dist.get_rank()]))
         else:
             self.total = lin.size()
             rank, world = (dist.get_rank(), dist.get_world_size()) if dist else (0, 1)

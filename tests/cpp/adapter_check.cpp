@@ -633,11 +633,15 @@ static bool check_fit(const char* what, const MODEL& init, const MODEL& referenc
   const LIN lin(bbm::vec2d<bbm::Size_t<C>>(12, 8), bbm::vec2d<bbm::Size_t<C>>(10, 6));
   const ERR err;
   bool ok = true;
-  double worst = 0;
+  double worst = 0, scale = 0;
+  std::string failed;
+  auto need = [&](bool c, const char* what) { if(!c && failed.find(what) == std::string::npos) failed += std::string(failed.empty() ? "" : ",") + what; ok &= c; };
+  // per-sample losses: 1e-5 relative, or within 1e-6 of the mean loss where a log loss cancels to ~0; 0 exactly 0
   auto rel = [&](double g, double w) {
+    if(std::isnan(g) || std::isnan(w)) return std::isnan(g) && std::isnan(w);   // NaN where the reference's is NaN
     const double e = (w == 0) ? (g == 0 ? 0.0 : 1.0) : std::fabs(g - w) / std::fabs(w);
     worst = std::max(worst, e);
-    return e <= 1e-5;
+    return e <= 1e-5 || (w != 0 && std::fabs(g - w) <= 1e-6 * scale);
   };
   // per-sample and total
   MODEL fr = init, fg = init;
@@ -645,12 +649,21 @@ static bool check_fit(const char* what, const MODEL& init, const MODEL& referenc
   bbm::hip::sampledlossfunction<MODEL> gf(fg, reference, err, lin);
   static_assert(bbm::concepts::sampledlossfunction<bbm::hip::sampledlossfunction<MODEL>>);
   const size_t n = rf.samples();
-  ok &= (gf.samples() == n);
+  need(gf.samples() == n, "samples");
   double want = 0;
-  for(size_t i = 0; i < n; ++i) want += double(rf(i));
-  for(size_t i = 0; i < n; i += 97) ok &= rel(double(gf(i)), double(rf(i)));
-  ok &= (gf(n) == 0) && (gf(n + 5) == 0);
-  ok &= rel(double(gf()), want / double(n));
+  for(size_t i = 0; i < n; ++i) { want += double(rf(i)); scale += std::fabs(double(rf(i))); }
+  scale /= double(n);
+  for(size_t i = 0; i < n; i += 97)
+  {
+    const double g = double(gf(i)), w = double(rf(i));
+    if(!rel(g, w))
+    {
+      std::fprintf(stderr, "%s: sample %zu gpu %.9g ref %.9g\n", what, i, g, w);
+      need(false, "per_sample");
+    }
+  }
+  need((gf(n) == 0) && (gf(n + 5) == 0), "masked_index");
+  need(rel(double(gf()), want / double(n)), "total");
   // compass: the batched GPU compass vs the reference's compass, step by step (not for a nested aggregate: the
   // reference cannot reflect its parameters as one vector, util/reflection.h:247, so its compass cannot hold them)
   int same = 0;
@@ -670,10 +683,13 @@ static bool check_fit(const char* what, const MODEL& init, const MODEL& referenc
       bool eq = true;
       for(size_t k = 0; k < pa.size(); ++k) eq &= (V(pa[k]) == V(pb[k])) && (V(pa[k]) == V(pc[k]));
       if(!eq) break;
-      ok &= rel(double(lb), double(la)) && (lb == lc);
+      // la: the reference's serial float total (float summation error, ~1e-5 here); lb / lc: the GPU's double sums,
+      // one batched launch vs one launch per probe -- the same sums bit for bit
+      need(std::fabs(double(lb) - double(la)) <= 1e-4 * std::fabs(double(la)), "compass_loss");
+      need(lb == lc, "compass_batched_vs_serial");
       ++same;
     }
-    ok &= (same == steps);
+    need(same == steps, "compass_trajectory");
   }
   // batch: the same indices, the same per-sample losses, after construction and after each update
   {
@@ -683,20 +699,22 @@ static bool check_fit(const char* what, const MODEL& init, const MODEL& referenc
     for(int u = 0; u < 3; ++u)
     {
       if(u) { rb.update(); gbt.update(); }
-      for(size_t i = 0; i < 200; i += 7) ok &= rel(double(gbt(i)), double(rb(i)));
+      for(size_t i = 0; i < 200; i += 7) need(rel(double(gbt(i)), double(rb(i))), "batch_per_sample");
       double bw = 0;
       for(size_t i = 0; i < 200; ++i) bw += double(rb(i));
-      ok &= rel(double(gbt()), bw / 200.0);
+      need(rel(double(gbt()), bw / 200.0), "batch_mean");
     }
   }
   // a one-rank RCCL communicator: the all-reduced sums are the shard's own
   {
     bbm::hip::comm cm(bbm::hip::comm::unique_id(), 0, 1);
     bbm::hip::sampledlossfunction<MODEL> gcm(fg, reference, err, lin, &cm);
-    ok &= (gcm() == gf());
+    const V a = gcm(), b = gf();
+    need(a == b || (std::isnan(a) && std::isnan(b)), "comm");
   }
   std::printf("{\"check\": \"fit_api\", \"model\": \"%s\", \"samples\": %zu, \"compass_steps_identical\": %d, "
-              "\"max_rel_err\": %.3e, \"ok\": %s}\n", what, n, same, worst, ok ? "true" : "false");
+              "\"max_rel_err\": %.3e, \"failed\": \"%s\", \"ok\": %s}\n", what, n, same, worst, failed.c_str(),
+              ok ? "true" : "false");
   return ok;
 }
 

@@ -158,3 +158,53 @@ def test_sharded_compass_two_ranks_gloo():
         assert p.exitcode == 0
     np.testing.assert_array_equal(res[0], res[1])
     np.testing.assert_array_equal(res[0], single)
+
+
+def _pairs_dist_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from bbm_amd import fit
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 5 + 3 * rank                                  # ranks hold different numbers of their own pairs
+        d = torch.zeros((3, n), dtype=torch.float32)
+        loss = fit.SampledLoss(_model("Aggregate<Lambertian,CookTorrance>"), torch.zeros((3, n)), "standardLog",
+                               pairs=(d, d), dist=dist)
+        # stand-in for the device launch: every local sample contributes 1 to each probe's sum
+        loss.local_sums = lambda probes: torch.full((len(probes),), float(n), dtype=torch.float64)
+        q.put((rank, loss.total, loss.begin, loss.n, loss.probe_losses(np.zeros((2, 4), np.float32)).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_own_pairs_two_ranks_gloo():
+    """SampledLoss(pairs=..., dist=...) with world size 2 (gloo): each rank's own pairs are its part of the grid, so
+    total is the sum of the ranks' counts, begin the lower ranks' count, and the mean loss divides the all-reduced
+    sums by that total (a mean of 1 per sample stays 1)."""
+    import multiprocessing as mp
+    import queue
+    import socket
+    import time
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pairs_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res, t0 = {}, time.time()
+    while len(res) < len(procs):
+        try:
+            r = q.get(timeout=2)
+            res[r[0]] = r[1:]
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a rank died (exit codes {dead})"
+            assert time.time() - t0 < 300, "ranks did not finish"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][:3] == (13, 0, 5) and res[1][:3] == (13, 5, 8)
+    assert res[0][3] == res[1][3] == [1.0, 1.0]

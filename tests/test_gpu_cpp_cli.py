@@ -90,7 +90,7 @@ def test_sample_and_symmetry_match_python_driver(bbm):
     chi = [l for l in out.splitlines() if l.startswith(" Chi2 for ")]
     assert len(chi) == 2
     for k, l in enumerate(chi):
-        v = _nums(l)
+        v = _nums(l[len(" Chi2 for "):])
         _same(v[3], res["trials"][k]["chi2"])
         assert int(v[4]) == res["trials"][k]["df"]
     out = _run(f"bsdfmodel={m}", "test=reciprocity", "samples=100000")

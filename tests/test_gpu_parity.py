@@ -36,14 +36,17 @@ TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
 MAX_EXCUSED_FRAC = 1e-3       # at most this fraction of a batch's lanes may need an input-ulps proof
 MAX_SAMPLER_FRAC = 0.05       # ... a sampler-CDF proof (a CDF entry moves the ~2/90 of directions in its bins)
 # Ceiling on the relative error of the lanes that pass by a proof (the proofs bound WHY a lane differs, this bounds
-# HOW MUCH): the ill-conditioned lanes of the cancelling models -- Bagher's shadowing 1 + Lambda (1 - e^(c t^k))
-# and the He family's series at tiny D -- reach ~1e-2 at their fitted parameters (profiles/r02_parity_large_0*.json);
-# every other model stays below 1e-3.  A kernel regression confined to ill-conditioned lanes would exceed these.
-# round 3: Bagher / Aggregate(Lambertian, Bagher) 5e-2, the He family 2e-2; round 4 (glibc powf / expf / logf / erfcf
-# restated, the measured tail: Bagher 2.9e-3, Aggregate(Lambertian, Bagher) 1.6e-2 on one lane where the Lambertian
-# and a negative Bagher Fresnel term cancel, HeWestin 2.3e-4): the He family under the default ceiling
-EXCUSED_REL_CEILING = {"Bagher": 5e-3, "Aggregate<Lambertian,Bagher>": 2e-2}
-EXCUSED_REL_DEFAULT = 1e-3
+# HOW MUCH).  History: round 3 Bagher / Aggregate(Lambertian, Bagher) 5e-2 and the He family 2e-2 (the ill-conditioned
+# lanes of Bagher's shadowing 1 + Lambda (1 - e^(c t^k)) and of He's series at tiny D); round 4 (glibc powf / expf /
+# logf / erfcf restated) Bagher 5e-3, Aggregate(Lambertian, Bagher) 2e-2, the rest 1e-3.  Round 5 (Bagher's D by
+# glibc's powf / expf in every mode): Aggregate(Lambertian, Bagher) bit-identical on both 1M-pair batches, no proven
+# lane of any model at or above TINY off by more than 1.7e-5 (HeWestin; profiles/r05_parity_*.json) -- one ceiling
+# for all.  Below TINY the default mode rounds quotients of subnormal intermediates on the normal grid
+# (set_exact_subnormals), and Bagher's proven lanes there reach 5.3e-3 on values ~1e-36: TINY_REL_CEILING.
+EXCUSED_REL_CEILING = {}
+EXCUSED_REL_DEFAULT = 1e-4
+TINY = 1e-30
+TINY_REL_CEILING = 1e-2
 
 
 @pytest.fixture(scope="module")
@@ -103,11 +106,17 @@ def check_lanes(got, ref, what, provers=(), model=None):
     assert bad.size - n_sampler <= max(2, MAX_EXCUSED_FRAC * n), \
         f"{what}: {bad.size - n_sampler} of {n} lanes needed an input-ulps proof ({proven})"
     assert n_sampler <= max(2, MAX_SAMPLER_FRAC * n), f"{what}: {n_sampler} of {n} lanes needed a sampler-CDF proof"
-    excused = ou.max_rel_normal(got[..., bad], ref[..., bad]) if bad.size else 0.0
+    gb, rb = got[..., bad], ref[..., bad]
+    big = np.abs(rb) >= TINY
+    excused = ou.max_rel_normal(np.where(big, gb, rb), rb) if bad.size else 0.0
+    excused_tiny = ou.max_rel_normal(np.where(big, rb, gb), rb) if bad.size else 0.0
     ceiling = EXCUSED_REL_CEILING.get(model or what.split("[")[0].split(" ")[0].split("/")[0], EXCUSED_REL_DEFAULT)
     assert excused <= ceiling, f"{what}: a proven lane is {excused:.3e} off (ceiling {ceiling:g})"
+    assert excused_tiny <= TINY_REL_CEILING, \
+        f"{what}: a proven lane below {TINY:g} is {excused_tiny:.3e} off (ceiling {TINY_REL_CEILING:g})"
     sub = (np.abs(ref) < ou.FLT_MIN) & (ref != 0)
     return {"lanes": int(n), "max_rel_normal": ou.max_rel_normal(got, ref), "max_rel_proven": excused,
+            "max_rel_proven_below_tiny": excused_tiny,
             "max_ulp": int(ou.ulp_diff(got, ref).max()) if got.size else 0,
             "frac_bit_exact": float(np.mean(ou.ulp_diff(got, ref) == 0)) if got.size else 1.0,
             "subnormal_ref_values": int(sub.sum()), "lanes_outside_bar": int(bad.size),
