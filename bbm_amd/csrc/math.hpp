@@ -9,6 +9,15 @@
 // The whole TU is compiled with -ffp-contract=off: every float op rounds on its own, exactly as
 // the reference's x86-64 build does, so results match the CPU backbone to ~1 ulp (transcendentals
 // are the only non-correctly-rounded ops on either side).
+//
+// Third-party notices (THIRD_PARTY_NOTICES.md has the full texts).  The float libm restatements below follow glibc 2.35
+// (GNU C Library, LGPL-2.1-or-later), whose expf / logf / powf / sinf / cosf come from Arm's optimized-routines
+// (Copyright (c) 2017-2018 Arm Ltd; MIT OR Apache-2.0 WITH LLVM-exception upstream) and whose erff / erfcf / atan2f come
+// from Sun's fdlibm:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely granted, provided that this notice
+//   is preserved.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
