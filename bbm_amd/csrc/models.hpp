@@ -75,6 +75,16 @@ using CookTorranceHeitzM = Microfacet<Beckmann<true, true>, HeightCorrelated, Fr
 using GGXHeitzM = Microfacet<GGX<true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;                     // bsdfmodel/ggxheitz.h:28-34
 using NganCookTorranceM = Microfacet<Beckmann<false, true>, VGroove, FresnelSchlick, Norm::Cook, true>;         // bsdfmodel/ngan.h:141-147
 using PhongWalterM = Microfacet<PhongNdf, Uncorrelated, FresnelCook, Norm::Walter, true>;                         // bsdfmodel/phongwalter.h:27-33
+#ifdef BBM_HIP_MIDTIER_WAVES   // A/B: the mid-tier microfacet variants' occupancy
+template<> struct eval_waves<CookTorranceWalterM> { static constexpr int value = BBM_HIP_MIDTIER_WAVES; };
+template<> struct eval_waves<CookTorranceHeitzM> { static constexpr int value = BBM_HIP_MIDTIER_WAVES; };
+template<> struct eval_waves<PhongWalterM> { static constexpr int value = BBM_HIP_MIDTIER_WAVES; };
+#endif
+#ifdef BBM_HIP_MIDTIER_NOPF     // A/B: their first-quad prefetch
+template<> struct eval_prefetch<CookTorranceWalterM> { static constexpr bool value = false; };
+template<> struct eval_prefetch<CookTorranceHeitzM> { static constexpr bool value = false; };
+template<> struct eval_prefetch<PhongWalterM> { static constexpr bool value = false; };
+#endif
 using RibardiereM = Microfacet<StudentT<false>, Uncorrelated, FresnelCook, Norm::Walter, true>;                   // bsdfmodel/ribardiere.h:28-34
 using RibardiereAnisoM = Microfacet<StudentT<true>, Uncorrelated, FresnelCook, Norm::Walter, true>;              // bsdfmodel/ribardiere.h:46-52
 

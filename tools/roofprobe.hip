@@ -50,7 +50,12 @@ __global__ __launch_bounds__(256) void k_probe(Args a)
     s.x += v[3].x; s.y += v[4].y; s.z += v[5].z; s.w += v[1].w + v[2].x;
     if (V == 3)
     {
-      if (s.x == 12345.678f) a.out[0][t] = s;   // keep loads live; never true for unit vectors
+      // keep every loaded float live (round 4's form tested s.x alone, so the compiler dropped 4 of the 6 streams'
+      // loads and the variant reported 19.2 TB/s); never true for unit vectors
+      float all = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) all += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+      if (all == 12345.678f) a.out[0][t] = s;
       continue;
     }
     if (V == 1)
@@ -114,9 +119,10 @@ __global__ __launch_bounds__(256) void k_probe2(Args a)
     f4 v[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) v[k] = __builtin_nontemporal_load(&a.in[k][t]);
-    f4 s = v[0];
-    s.x += v[3].x; s.y += v[4].y; s.z += v[5].z; s.w += v[1].w + v[2].x;
-    if (s.x == 12345.678f) a.out[0][t] = s;
+    float all = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) all += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    if (all == 12345.678f) a.out[0][t] = v[0];     // every loaded float live (see variant 3)
   }
 }
 

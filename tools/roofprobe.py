@@ -3,7 +3,8 @@
 
     python tools/roofprobe.py [--pairs 100000000]
 
-Prints one line per (variant, grid) with GB/s computed from the algorithmic bytes.
+Prints one line per (variant, grid) with GB/s computed from the algorithmic bytes.  Build the probe library with
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -o tools/libroofprobe.so tools/roofprobe.hip
 """
 import argparse
 import ctypes
