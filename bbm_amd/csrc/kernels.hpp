@@ -139,6 +139,12 @@ template<class Model> struct eval_prefetch { static constexpr bool value = false
 template<class Model> struct eval_prefetch { static constexpr bool value = true; };
 #endif
 
+// Software pipelining of k_eval_pdf_v4's grid-stride loop: the next quad's six loads are issued before the current
+// quad is evaluated, so a thread's HBM latency hides under its own compute (with a capped grid, eval_grid_cap, every
+// thread runs several iterations).  For the latency-bound models whose waves otherwise all wait on their loads at
+// the same time.
+template<class Model> struct eval_pipeline { static constexpr bool value = false; };
+
 // Grid cap of the eval kernels (0 = a full grid, one workgroup per 1024 pairs).  The model is constructed once per
 // thread from the kernarg parameters; where that constructor is expensive (the Student-T NDF's two tgamma and a pow
 // per thread) a capped grid-stride launch amortises it over several iterations.
@@ -160,13 +166,24 @@ void k_eval_pdf_v4(EvalArgs a)
     ox = ld4<NT>(a.ox, q); oy = ld4<NT>(a.oy, q); oz = ld4<NT>(a.oz, q);
     if (MASK) mk = reinterpret_cast<const uint32_t*>(a.mask)[q];
   };
-  constexpr bool pf = eval_prefetch<Model>::value;
+  constexpr bool pipe = eval_pipeline<Model>::value;
+  constexpr bool pf = eval_prefetch<Model>::value || pipe;
   if (pf && t < n4) load(t);
   math_tables_init();
   const Model m(a.p.v);
   for (bool first = true; t < n4; t += stride, first = false)
   {
-    if (!pf || !first) load(t);
+    float4 nix, niy, niz, nox, noy, noz;
+    uint32_t nmk = 0x01010101u;
+    if constexpr (pipe)
+    {
+      // the next iteration's quad (clamped: every lane loads, the last iteration's loads are discarded)
+      const uint64_t q = (t + stride < n4) ? t + stride : t;
+      nix = ld4<NT>(a.ix, q); niy = ld4<NT>(a.iy, q); niz = ld4<NT>(a.iz, q);
+      nox = ld4<NT>(a.ox, q); noy = ld4<NT>(a.oy, q); noz = ld4<NT>(a.oz, q);
+      if (MASK) nmk = reinterpret_cast<const uint32_t*>(a.mask)[q];
+    }
+    else if (!pf || !first) load(t);
     const float inx[4] = {ix.x, ix.y, ix.z, ix.w}, iny[4] = {iy.x, iy.y, iy.z, iy.w}, inz[4] = {iz.x, iz.y, iz.z, iz.w};
     const float onx[4] = {ox.x, ox.y, ox.z, ox.w}, ony[4] = {oy.x, oy.y, oy.z, oy.w}, onz[4] = {oz.x, oz.y, oz.z, oz.w};
     float r[4], g[4], b[4], p[4];
@@ -185,6 +202,11 @@ void k_eval_pdf_v4(EvalArgs a)
       st4<NT>(a.b, t, b[0], b[1], b[2], b[3]);
     }
     if (MODE & kModePdf) st4<NT>(a.pdf, t, p[0], p[1], p[2], p[3]);
+    if constexpr (pipe)
+    {
+      ix = nix; iy = niy; iz = niz; ox = nox; oy = noy; oz = noz;
+      mk = nmk;
+    }
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3))

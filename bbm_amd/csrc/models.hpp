@@ -80,6 +80,14 @@ template<> struct eval_waves<CookTorranceWalterM> { static constexpr int value =
 template<> struct eval_waves<CookTorranceHeitzM> { static constexpr int value = BBM_HIP_MIDTIER_WAVES; };
 template<> struct eval_waves<PhongWalterM> { static constexpr int value = BBM_HIP_MIDTIER_WAVES; };
 #endif
+#ifdef BBM_HIP_MIDTIER_PIPE     // A/B: software-pipelined loop on a capped grid
+template<> struct eval_pipeline<CookTorranceWalterM> { static constexpr bool value = true; };
+template<> struct eval_pipeline<CookTorranceHeitzM> { static constexpr bool value = true; };
+template<> struct eval_pipeline<PhongWalterM> { static constexpr bool value = true; };
+template<> struct eval_grid_cap<CookTorranceWalterM> { static constexpr uint64_t value = BBM_HIP_MIDTIER_PIPE; };
+template<> struct eval_grid_cap<CookTorranceHeitzM> { static constexpr uint64_t value = BBM_HIP_MIDTIER_PIPE; };
+template<> struct eval_grid_cap<PhongWalterM> { static constexpr uint64_t value = BBM_HIP_MIDTIER_PIPE; };
+#endif
 #ifdef BBM_HIP_MIDTIER_NOPF     // A/B: their first-quad prefetch
 template<> struct eval_prefetch<CookTorranceWalterM> { static constexpr bool value = false; };
 template<> struct eval_prefetch<CookTorranceHeitzM> { static constexpr bool value = false; };

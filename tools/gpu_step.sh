@@ -18,6 +18,9 @@ R="$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 SQ8="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64"
 LANE="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES"
+# PMC_WAIT=1: a third pass -- where the wave cycles go (parked on s_waitcnt, issue-stalled, issuing) and the
+# GPU-busy cycles (GRBM_GUI_ACTIVE / dispatch time = the clock the kernel ran at)
+WAIT="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
 
 step_tests() {
   local k=()
@@ -70,7 +73,9 @@ step_pmc() {
       models) sel=(--models "$M" --graph off);;
       sample) sel=(--models "$M" --no-exact);;    # the default sampler, not the exact-mode twin timed after it
     esac
-    for P in "$SQ8" "$LANE"; do
+    local passes=("$SQ8" "$LANE")
+    [ -n "$PMC_WAIT" ] && passes+=("$WAIT")
+    for P in "${passes[@]}"; do
       local tag
       tag=$(echo $P | cut -d' ' -f1)-$(echo $P | wc -w)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --pmc $P --kernel-trace --output-format csv \
@@ -86,6 +91,10 @@ v = c.get("SQ_INSTS_VALU", 0)
 print(sys.argv[3], "valu/unit %.0f" % (v * 64 / u), "issue %.3f" % (v / (c["dispatch_ns"] * 1e-9 * 1.2288e12)),
       "lane %.3f" % (c.get("SQ_THREAD_CYCLES_VALU", 0) / max(64 * c.get("SQ_ACTIVE_INST_VALU", 1), 1)),
       "f64fma %.0f" % (c.get("SQ_INSTS_VALU_FMA_F64", 0) * 64 / u), "ms %.4f" % (c["dispatch_ns"] / 1e6))
+if "SQ_WAIT_ANY" in c:
+    w = max(c.get("SQ_WAVE_CYCLES", 1), 1)
+    print("   wait %.3f inst-stall %.3f active %.3f  clock %.2f GHz" % (c["SQ_WAIT_ANY"] / w, c["SQ_WAIT_INST_ANY"] / w,
+          c["SQ_ACTIVE_INST_ANY"] / w, c.get("GRBM_GUI_ACTIVE", 0) / c["dispatch_ns"]))
 EOF
     rm -rf "${out:?}/$M"/*/   # raw CSVs: the summary above is what is kept
   done
