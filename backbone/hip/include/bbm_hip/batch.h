@@ -538,6 +538,11 @@ namespace bbm {
     //! pdf differently and sample differently: the wrapped object decides -- an aggregatebsdf keeps the parser's
     //! runtime semantics (its children are the bsdf_ptrs its string describes), anything else is a template
     //! model, aggregatemodel at every level.
+    //! Limitation: only the root is inspected.  Below a runtime root every aggregate child keeps runtime semantics,
+    //! also one whose bsdf_ptr wraps a template bsdf<aggregatemodel<...>> (the string alone cannot tell them apart
+    //! and aggregatebsdf exposes no accessor for its children); such a child's pdf rounding and its sum <= eps
+    //! sampling rule then follow aggregatebsdf.  Build that child from its model type (describe(model)) where it
+    //! matters.
     template<typename C>
       inline model_desc describe(const bbm::bsdf_ptr<C>& ptr)
     {

@@ -715,9 +715,14 @@ def tree_desc(model, f64=False):
 def Aggregate(*children, fused=True, runtime=False):
     """aggregate(models...) (aggregatemodel.h:232-233): the fused kernel for the published fits' form
     Aggregate(Lambertian, X) where one is registered (fused=False forces the composed path), otherwise an
-    AggregateModel over the children's own kernels.  runtime=True: the reference's runtime aggregatebsdf
-    (aggregatebsdf.h, the aggregate of bsdf_ptrs that fromString / bsdf_import / checkBsdf build) instead of
-    aggregatemodel<...> -- same eval for two children, but the pdf's and sample's own rounding and rules."""
+    AggregateModel over the children's own kernels.
+
+    Note: this mirrors the C++ template aggregate() (aggregatemodel<...>), NOT the reference's Python binding
+    bbm.Aggregate (include/python/py_core.h:116-123), which builds the runtime aggregatebsdf of bsdf_ptrs.  The two
+    differ in the pdf's rounding (inner product / sum here, per-term there) and in sampling (here a child is sampled
+    even when the weights sum below eps).  Scripts ported from the reference's Python API get the binding's
+    semantics with runtime=True, or with fromString("Aggregate(...)"), which returns runtime aggregates like
+    bsdf_import does."""
     key = aggregate_key([c.name for c in children])
     if fused and key in AGGREGATES and all(isinstance(c, BsdfModel) for c in children):
         m = BsdfModel(key, *children)

@@ -75,14 +75,25 @@ size_t free_idle(bool wait, size_t keep)
 }
 }  // namespace
 
+thread_local std::string g_scratch_why;
+
+std::string scratch_failure() { return g_scratch_why.empty() ? std::string("out of device memory") : g_scratch_why; }
+
 void* scratch_acquire(size_t bytes, hipStream_t s)
 {
+  g_scratch_why.clear();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   bytes = (bytes + 255) & ~size_t(255);
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return nullptr;
+  if (const hipError_t e = hipStreamIsCapturing(s, &cap); e != hipSuccess)
+  {
+    // e.g. the legacy null stream while another stream is under a global-mode capture
+    g_scratch_why = std::string("the stream's capture status cannot be read (hipStreamIsCapturing: ") +
+                    hipGetErrorString(e) + "; a call on the null stream during a global-mode capture?)";
+    return nullptr;
+  }
   if (cap != hipStreamCaptureStatusNone)
   {
     // graph capture: a fresh block that belongs to the graph from now on.  No idle block is reused (its release

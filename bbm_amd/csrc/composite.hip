@@ -239,7 +239,7 @@ template<> struct Leaf<double>
   {
     Scratch sc(s);
     double* p = sc.get<double>(n);
-    if (!p) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+    if (!p) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
     return bbm_hip_eval_pdf_f64(c.model_id, c.params, c.nparams, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, r, g, b,
                                 p, s);
   }
@@ -251,7 +251,7 @@ template<> struct Leaf<double>
     double* r = sc.get<double>(n);
     double* g = sc.get<double>(n);
     double* b = sc.get<double>(n);
-    if (!r || !g || !b) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+    if (!r || !g || !b) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
     return bbm_hip_eval_pdf_f64(c.model_id, c.params, c.nparams, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, r, g, b,
                                 p, s);
   }
@@ -421,7 +421,7 @@ struct Composite
     T* tr = sc.get<T>(n);
     T* tg = sc.get<T>(n);
     T* tb = sc.get<T>(n);
-    if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+    if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
     int rc;
     if (r && (rc = fold(nchild, bsdf, n, r, g, b, tr, tg, tb, s, [&](int k, T* rr, T* gg, T* bb) {
           return child_eval(c[k], ix, iy, iz, ox, oy, oz, mask, n, comp, unit, rr, gg, bb, s);
@@ -432,7 +432,7 @@ struct Composite
       T* w = sc.get<T>(size_t(nchild) * n);
       T* sum = sc.get<T>(n);
       T* ip = sc.get<T>(n);
-      if (!w || !sum || !ip) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+      if (!w || !sum || !ip) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
       if ((rc = weights(c, nchild, ox, oy, oz, mask, n, comp, unit, w, sum, tr, tg, tb, s))) return rc;
       if ((rc = mixture_pdf(c, nchild, bsdf, ix, iy, iz, ox, oy, oz, mask, n, comp, unit, w, sum, tr, ip, pdf, s)))
         return rc;
@@ -447,7 +447,7 @@ struct Composite
     T* tr = sc.get<T>(n);
     T* tg = sc.get<T>(n);
     T* tb = sc.get<T>(n);
-    if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+    if (!tr || !tg || !tb) return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
     return fold(nchild, bsdf, n, r, g, b, tr, tg, tb, s, [&](int k, T* rr, T* gg, T* bb) {
       return child_reflectance(c[k], ox, oy, oz, mask, n, comp, unit, rr, gg, bb, s);
     });
@@ -470,7 +470,7 @@ struct Composite
     uint8_t* cm = sc.get<uint8_t>(n);
     T* xs = sc.get<T>(n);
     if (!w || !sum || !ip || !t0 || !t1 || !t2 || !t3 || !tf || !chosen || !cm || !xs)
-      return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed");
+      return fail(BBM_HIP_ERR_HIP, "aggregate: scratch allocation failed: " + scratch_failure());
     int rc;
     if ((rc = weights(c, nchild, ox, oy, oz, mask, n, comp, unit, w, sum, t0, t1, t2, s))) return rc;
     hipLaunchKernelGGL(k_select<T>, dim3(grid(n)), dim3(kB), 0, s, w, nchild, sum, xi0, mask, chosen, xs, uint64_t(n),
@@ -651,7 +651,7 @@ int loss_tree(const typename Leaf<T>::Child* tree, int ntree, const T* probes, i
   }
   Scratch sc(s);
   T* rgb = sc.get<T>(3 * n);
-  if (!rgb) return fail(BBM_HIP_ERR_HIP, "loss: scratch allocation failed");
+  if (!rgb) return fail(BBM_HIP_ERR_HIP, "loss: scratch allocation failed: " + scratch_failure());
   for (int p = 0; p < nprobes; ++p)
   {
     std::vector<std::vector<Child>> store;
@@ -934,10 +934,10 @@ int check_tree_test(const Model<T>& m, const bbm_hip_check_desc* d, const T* sx,
   Scratch sc(s);
   T* buf[22];
   for (T*& q : buf)
-    if (!(q = sc.get<T>(lanes))) return fail(BBM_HIP_ERR_HIP, "check: scratch allocation failed");
+    if (!(q = sc.get<T>(lanes))) return fail(BBM_HIP_ERR_HIP, "check: scratch allocation failed: " + scratch_failure());
   uint32_t* fa = sc.get<uint32_t>(lanes);
   uint32_t* fb = sc.get<uint32_t>(lanes);
-  if (!fa || !fb) return fail(BBM_HIP_ERR_HIP, "check: scratch allocation failed");
+  if (!fa || !fb) return fail(BBM_HIP_ERR_HIP, "check: scratch allocation failed: " + scratch_failure());
   T *ax = buf[0], *ay = buf[1], *az = buf[2], *bx = buf[3], *by = buf[4], *bz = buf[5], *x0 = buf[6], *x1 = buf[7];
   T *y0 = buf[8], *y1 = buf[9], *aux = buf[10], *r = buf[11], *g = buf[12], *b = buf[13], *r2 = buf[14];
   T *g2 = buf[15], *b2 = buf[16], *pa = buf[17], *pb = buf[18], *qa = buf[19], *qb = buf[20], *cz = buf[21];

@@ -9,6 +9,7 @@
 namespace bbmhip {
 
 int fail(int code, const std::string& msg);
+std::string scratch_failure();
 
 namespace f64 {
 namespace {
@@ -175,7 +176,7 @@ struct host_params<He<FRES, ERRATA, WESTIN, TAYLOR, ADAPTIVE, APPROX, SCALED>>
   static int run(ParamBlockF64& p, uint32_t component, hipStream_t s, void** scratch)
   {
     double* cdf = static_cast<double*>(scratch_acquire(90 * sizeof(double), s));
-    if (!cdf) return fail(BBM_HIP_ERR_HIP, "He (f64) sampler CDF: scratch allocation failed");
+    if (!cdf) return fail(BBM_HIP_ERR_HIP, "He (f64) sampler CDF: scratch allocation failed: " + scratch_failure());
     *scratch = cdf;
     hipLaunchKernelGGL((k_he_cdf_f64<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
     if (const int rc = launched("k_he_cdf_f64")) return rc;

@@ -618,7 +618,7 @@ template<class M>
 int ndf_sampler_cdf_run(ParamBlock& p, uint32_t component, hipStream_t s, void** scratch, const char* who)
 {
   float* cdf = static_cast<float*>(scratch_acquire(kHeBins * sizeof(float), s));
-  if (!cdf) return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: scratch allocation failed");
+  if (!cdf) return fail(BBM_HIP_ERR_HIP, std::string(who) + " sampler CDF: scratch allocation failed: " + scratch_failure());
   hipError_t e;
   hipLaunchKernelGGL((k_he_cdf<M>), dim3(1), dim3(128), 0, s, p, component, cdf);
   if ((e = hipGetLastError()) != hipSuccess)

@@ -38,6 +38,7 @@ int fail(int code, const std::string& msg);
 // hipMallocAsync / hipFreeAsync on the caller's stream, under which tests/cpp/adapter_check -- a plain C++
 // host program on the null stream -- saw He CDFs and composed-aggregate outputs corrupted at random.)
 void* scratch_acquire(size_t bytes, hipStream_t s);
+std::string scratch_failure();   // why the calling thread's last scratch_acquire returned nullptr
 void scratch_release(void* p, hipStream_t s);
 
 struct ParamBlock { float v[kMaxParams]; };

@@ -264,8 +264,10 @@ __device__ __forceinline__ float expf_rn(float x) { return exp2_cr(double(x) * 1
 // IEEE double ops: x N / ln2 = k + r (N = 32), 2^(k/N) from a 32-entry table of doubles plus an exponent shift,
 // 2^(r/N) by a cubic, one final rounding to float.  The x86-64 library is the ifunc variant built with FMA
 // contraction (__expf_fma on any FMA-capable host): r = fma(InvLn2N, x, -kd) and the cubic's three FMAs.  This
-// restatement returns the same float as the container's libm for EVERY float in [-110, 90] (2.24e9 inputs,
-// oracle/expf_glibc_check.c); outside that range glibc's special cases (0, inf, NaN) are mirrored by selects.
+// restatement's steps, transcribed to host C (oracle/expf_glibc_check.c), return the same float as the container's
+// libm for EVERY float in [-110, 90] (2.24e9 inputs); the device code itself is pinned by strided GPU sweeps of the
+// bit patterns against the host libm (tests/test_gpu_libm.py).  Outside that range glibc's special cases (0, inf,
+// NaN) are mirrored by selects.
 // ~10 f64 VALU + a 64-bit table gather, branch-free: cheaper than exp2_cr's polynomial and exact to the bit.
 __device__ __constant__ const uint64_t kExpfTab[32] = {
     0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
@@ -379,8 +381,9 @@ __device__ __forceinline__ float expf_glibc_neg(float x)
 // variant the host runs.  Neither is correctly rounded (logf 0.82 ulp; powf carries up to 1.27 2^-26 relative error
 // into its one rounding, so ~0.1 % of its results are not the nearest float), and where the reference cancels
 // right after (Bagher's 1 - e^(c theta^k)) only glibc's own float reproduces its result.  The tables and polynomials
-// are glibc's data (as in this machine's libm.so.6), not the reference's.  Both are pinned to the host libm by
-// oracle/glibcf_check.c: logf on every positive float, powf on 1e9 random pairs -- 0 mismatches.
+// are glibc's data (as in this machine's libm.so.6), not the reference's.  A host C transcription of the same steps
+// (oracle/glibcf_check.c) matches the host libm for logf on every positive float and powf on 1e9 random pairs (0
+// mismatches); the device code is pinned by strided GPU sweeps against the host libm (tests/test_gpu_libm.py).
 __device__ __constant__ const double kLogfTab[16][2] = {    // {1/c, log c}
     {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
     {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
@@ -536,7 +539,8 @@ __device__ __forceinline__ float powf_glibc_pos(float x, float y)
 // bbm::erf / bbm::erfc of a float return (std::erf / std::erfc -> erff / erfcf).  Neither is correctly rounded; the
 // He family's shadowing term S1 subtracts erfc from a nearly equal quantity and the Beckmann VNDF sampler inverts
 // erf by Newton steps, so only glibc's own floats reproduce the reference there.  Coefficients: fdlibm's floats as
-// this machine's libm.so.6 holds them.  Pinned on all 2^32 inputs by oracle/erfcf_glibc_check.c (0 mismatches).
+// this machine's libm.so.6 holds them.  A host C transcription (oracle/erfcf_glibc_check.c) matches the host libm on
+// all 2^32 inputs (0 mismatches); the device code is pinned by strided GPU sweeps (tests/test_gpu_libm.py).
 namespace fdlibm_erf {
 constexpr float erx = 8.4506291151e-01f, pp0 = 1.2837916613e-01f, pp1 = -3.2504209876e-01f,
                 pp2 = -2.8481749818e-02f, pp3 = -5.7702702470e-03f, pp4 = -2.3763017452e-05f, qq1 = 3.9791721106e-01f,
@@ -649,8 +653,9 @@ __device__ __forceinline__ float erff_glibc(float x)
 // (atan 0.5, 1, 1.5, inf as hi + lo; one more IEEE division) and its 11-term odd polynomial, then the quadrant
 // fix-ups with pi_lo.  Not correctly rounded, hence restated rather than rounded from a double atan2.  Same float as
 // this machine's libm on 6e7 random pairs (unit-vector components, any finite floats, mixed magnitudes) and on every
-// combination of zeros, infinities and NaN, and at x = 1 (glibc's atanf shortcut, the same float) for every 13th y
-// (oracle/atan2f_glibc_check.c).  Selects around two IEEE divisions.
+// combination of zeros, infinities and NaN, and at x = 1 (glibc's atanf shortcut, the same float) for every 13th y --
+// measured on a host C transcription (oracle/atan2f_glibc_check.c); the device code by GPU sweeps against the host
+// libm (tests/test_gpu_libm.py).  Selects around two IEEE divisions.
 namespace fdlibm_atan {
 constexpr float kHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
 constexpr float kLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
@@ -717,8 +722,9 @@ __device__ __forceinline__ float atan2f_glibc(float y, float x)
 // / 1 below 2^-12); |y| < 120: the quadrant n from y (2/pi) 2^24 truncated (+2^23, >> 24), r = y - n pi/2 by one
 // FMA, sin(r) by the odd and cos(r) by the even polynomial, swapped in odd quadrants and signed per quadrant.  The
 // coefficients are glibc's table (__sincosf_table[0]; table [1] is its even half negated, which the sign select
-// reproduces exactly).  Every float |y| < 120 gives glibc's sinf and cosf bit for bit (oracle/sincosf_glibc_check.c,
-// all 2.2e9).  Larger |y|, inf and NaN (no sampler angle) take the device library's sincosf.
+// reproduces exactly).  A host C transcription of these steps (oracle/sincosf_glibc_check.c) gives glibc's sinf and
+// cosf bit for bit for every float |y| < 120 (all 2.2e9); the device code is pinned by a strided GPU sweep of that
+// domain (tests/test_gpu_libm.py).  Larger |y|, inf and NaN (no sampler angle) take the device library's sincosf.
 __device__ __forceinline__ void sincosf_glibc(float y, float* sp, float* cp)
 {
   constexpr double kC0 = 1.0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5, kC3 = -0x1.6c087e89a359dp-10,

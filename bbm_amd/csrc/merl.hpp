@@ -48,6 +48,87 @@ __device__ __forceinline__ uint32_t merl_index(v3 in, v3 out)
   return uint32_t((ihc * kMerlThetaD + itc) * kMerlPhiD + ipc);
 }
 
+// The same bin from a cheap evaluation, where it is provably the same.  The exact map above spends ~600 VALU per
+// pair on the reference's own floats (two glibc atan2f, two double asin thetas, two correctly rounded sincos) although
+// only the three floor()ed bin coordinates matter.  Here the half-vector frame comes from the halfway vector itself
+// (cos / sin of phi_h = half.xy / |half.xy|, of theta_h = half.z and |half.xy|: no angles), the difference vector d
+// from those, and the angles from the device library's asinf / atan2f (<= 2 ulp).  Every approximation differs from
+// the reference's float by a bounded amount: d by <= kMerlDErr per component (the reference's own cos / sin of
+// rounded angles against the geometric ones, ~3e-7, and the float rotations, with a margin), theta_d through
+// 2 asin(|d - pole| / 2) (slope <= sqrt2 for d.z >= 0), phi_d through atan2 (slope 1 / |d.xy|), theta_h only by the
+// asin (half and its chord are the reference's own floats).  A coordinate is decided where floor() takes the same
+// value over its whole error interval (plus two ulp of the float ops that form it, as the reference forms them);
+// phi_d also away from its fold points (raw atan2 at 0 and +-pi, where the reference's +2 pi / -pi moves the bin to
+// the other end).  Lanes not decided -- and NaN / degenerate frames -- set sure = false and take merl_index.
+constexpr float kMerlDErr = 4e-6f;
+
+__device__ __forceinline__ bool merl_floor_sure(float q, float e, float& f)
+{
+  const float lo = floorf(q - e), hi = floorf(q + e);
+  f = lo;
+  return lo == hi;
+}
+
+__device__ __forceinline__ uint32_t merl_index_fast(v3 in, v3 out, bool& sure)
+{
+  const v3 half = halfway(in, out);
+  const float rxy2 = (0.0f + half.x * half.x) + half.y * half.y;
+  const float rxy = sqrtf(rxy2);
+  // theta_h as theta_of(half) forms it (z >= 0): the chord is the reference's float, the asin the device's
+  const float dzh = half.z - 1.0f;
+  const float h_th = 2.0f * asinf(0.5f * sqrtf(rxy2 + dzh * dzh));
+  const float rinv = __builtin_amdgcn_rcpf(rxy);
+  const float cph = half.x * rinv, sph = half.y * rinv;        // cos / sin of phi_h
+  const float cth = half.z, sth = rxy;                         // cos / sin of theta_h
+  // t = Rz(-phi_h) in, d = Ry(-theta_h) t
+  const float tx = cph * in.x + sph * in.y;
+  const float ty = cph * in.y - sph * in.x;
+  const float dx = cth * tx - sth * in.z;
+  const float dy = ty;
+  const float dz = sth * tx + cth * in.z;
+  const float dxy = sqrtf(dx * dx + dy * dy);
+  // theta_d = 2 asin(|d - (0, 0, 1)| / 2) for d.z >= 0 (d.z = cos theta_d = in.half >= 0)
+  const float ddz = dz - 1.0f;
+  const float d_th = 2.0f * asinf(0.5f * sqrtf(dx * dx + dy * dy + ddz * ddz));
+  const float raw = atan2f(dy, dx);
+  const float e_phi = (1.5f * kMerlDErr) / dxy + 1.5e-6f;
+  const float e_th = 3.0f * kMerlDErr + 1e-6f;
+  float d_phi = (raw < 0) ? raw + kPi2F : raw;
+  const bool same = dot3(in, out) > 1.0f - kEpsF;              // the reference's phi_d = 0 (computed identically)
+  bool ok = same || ((fabsf(raw) > e_phi) && (kPiF - fabsf(raw) > e_phi));
+  if (same) d_phi = 0.0f;
+  if (d_phi >= kPiF) d_phi = d_phi - kPiF;
+  float ip, it, ih;
+  // q = (coord / range + eps) * samples: the error interval in bin units, plus two ulp of q for the float ops
+  const float qp = (__fdiv_rn(d_phi, kPiF) + kEpsF) * float(kMerlPhiD);
+  const float qt = (__fdiv_rn(d_th, kPiHalfF) + kEpsF) * float(kMerlThetaD);
+  const float xh = __fdiv_rn(h_th, kPiHalfF) + kEpsF;
+  const float qh = safe_sqrtf(xh) * float(kMerlThetaH);
+  ok = merl_floor_sure(qp, same ? 0.0f : e_phi * (float(kMerlPhiD) / kPiF) + 4e-5f, ip) && ok;
+  ok = merl_floor_sure(qt, e_th * (float(kMerlThetaD) / kPiHalfF) + 4e-5f, it) && ok;
+  // theta_h: only the asin differs (<= 3 ulp of h_th); d sqrt(x) = dx / (2 sqrt x)
+  const float e_xh = 6e-7f * xh + 2.4e-7f;
+  ok = merl_floor_sure(qh, (0.5f * float(kMerlThetaH)) * e_xh * __builtin_amdgcn_rsqf(fmaxf(xh, 1e-30f)) + 4e-5f, ih) && ok;
+  sure = ok && (rxy > 1e-6f) && (dxy > 1e-6f);                  // false for NaN as well
+  const int ipc = int(clampf(ip, 0.0f, float(kMerlPhiD - 1)));
+  const int itc = int(clampf(it, 0.0f, float(kMerlThetaD - 1)));
+  const int ihc = int(clampf(ih, 0.0f, float(kMerlThetaH - 1)));
+  return uint32_t((ihc * kMerlThetaD + itc) * kMerlPhiD + ipc);
+}
+
+// the bin of merl_index, by merl_index_fast where it decides it; -DBBM_HIP_MERL_EXACT_INDEX (A/B): always exact
+__device__ __forceinline__ uint32_t merl_bin(v3 in, v3 out)
+{
+#ifdef BBM_HIP_MERL_EXACT_INDEX
+  return merl_index(in, out);
+#else
+  bool sure;
+  uint32_t idx = merl_index_fast(in, out, sure);
+  if (!sure) idx = merl_index(in, out);
+  return idx;
+#endif
+}
+
 struct Merl
 {
   static constexpr int kParams = 2;                      // device address of the float4 table
@@ -74,7 +155,7 @@ struct Merl
     // the table check is wave-uniform; it only matters for probe vectors the host cannot see (fit loss)
     if (((component & kFlagAll) == kFlagAll) && (in.z >= 0) && (out.z >= 0) && table)
     {
-      const float4 v = table[merl_index(in, out)];
+      const float4 v = table[merl_bin(in, out)];
       rgb[0] = v.x; rgb[1] = v.y; rgb[2] = v.z;
     }
   }

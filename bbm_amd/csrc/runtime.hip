@@ -21,6 +21,7 @@
 
 namespace bbmhip {
 int fail(int code, const std::string& msg);
+std::string scratch_failure();
 void* scratch_acquire(size_t bytes, hipStream_t s);
 void scratch_release(void* p, hipStream_t s);
 }  // namespace bbmhip
@@ -133,7 +134,7 @@ int gather(const uint64_t* index, size_t count, uint64_t nsamples, const T* cons
   if (keep.size() > size_t(INT32_MAX)) return fail(BBM_HIP_ERR_INVALID_ARG, "batch too large");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   void* di = scratch_acquire(keep.size() * sizeof(uint64_t), s);
-  if (!di) return fail(BBM_HIP_ERR_HIP, "scratch allocation failed (gather indices)");
+  if (!di) return fail(BBM_HIP_ERR_HIP, "gather indices: scratch allocation failed: " + scratch_failure());
   hipError_t e = hipMemcpyAsync(di, keep.data(), keep.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s);
   if (e == hipSuccess)
   {

@@ -195,3 +195,28 @@ def test_scratch_held_by_captured_graph(bbm):
     del g
     torch.cuda.synchronize()
     bbm.scratch_trim_captured()
+
+
+def test_scratch_bounded_over_repeated_captures(bbm):
+    """Capture, replay, destroy and trim (bbm_hip_scratch_trim_captured) N times: the scratch a capture pins is
+    released with its graph, so the pool does not grow with the number of captures."""
+    n = 1 << 14
+    din = bbm.fill_directions(21, 0, 0, n, mode=1)
+    dout = bbm.fill_directions(21, 1, 0, n, mode=1)
+    m = bbm.Aggregate(bbm.CookTorrance(), bbm.GGX(), bbm.Lambertian(), fused=False)
+    rgb, pdf = torch.empty((3, n), device="cuda"), torch.empty(n, device="cuda")
+    sizes = []
+    for _ in range(6):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            m.eval_pdf(din, dout, rgb=rgb, pdf=pdf, stream=side)
+        g.replay()
+        torch.cuda.synchronize()
+        del g
+        torch.cuda.synchronize()
+        bbm.scratch_trim_captured()
+        bbm.scratch_trim()
+        sizes.append(bbm.scratch_bytes())
+    assert max(sizes) == min(sizes), f"scratch grew over captures: {sizes}"
