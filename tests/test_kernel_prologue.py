@@ -13,7 +13,7 @@ from tests import oracle_util as ou
 
 KERNEL = re.compile(r"__global__[^;{]*?\)\s*\{", re.S)
 # what may not precede the prologue: a model, an evaluation, a table function, a call into the device math
-BEFORE_INIT = re.compile(r"\bModel\s+\w+\s*[({]|\bm\.|model_|_glibc|eval(?!_prefetch)|sample|reflectance|loss")
+BEFORE_INIT = re.compile(r"\bModel\s+\w+\s*[({]|\bm\.|model_|_glibc|eval(?!_prefetch|_pipeline)|sample|reflectance|loss")
 EXEMPT = {"runtime.hip"}
 
 
