@@ -116,7 +116,11 @@ __device__ __forceinline__ uint32_t merl_index_fast(v3 in, v3 out, bool& sure)
   return uint32_t((ihc * kMerlThetaD + itc) * kMerlPhiD + ipc);
 }
 
-// the bin of merl_index, by merl_index_fast where it decides it; -DBBM_HIP_MERL_EXACT_INDEX (A/B): always exact
+// the bin of merl_index, by merl_index_fast where it decides it; -DBBM_HIP_MERL_EXACT_INDEX (A/B): always exact.
+// Measured (10 M random pairs, profiles/r05_ab_merl_index.txt): 0.1555 -> 0.138 ms; without the exact fallback (a
+// timing probe) 0.135, so the undecided lanes cost ~4 %.  What remains is the table gather: every random pair reads
+// a different line of the 23 MB table from the Infinity Cache.  0 lanes off the reference's bin on the 2 x 1 M
+// parity pairs + edge cases (tests/test_gpu_merl.py, MAX_FLIP_FRAC = 0).
 __device__ __forceinline__ uint32_t merl_bin(v3 in, v3 out)
 {
 #ifdef BBM_HIP_MERL_EXACT_INDEX
@@ -124,7 +128,9 @@ __device__ __forceinline__ uint32_t merl_bin(v3 in, v3 out)
 #else
   bool sure;
   uint32_t idx = merl_index_fast(in, out, sure);
+#ifndef BBM_HIP_MERL_PROBE_NOFALLBACK     // timing probe only: the undecided lanes keep the cheap bin
   if (!sure) idx = merl_index(in, out);
+#endif
   return idx;
 #endif
 }

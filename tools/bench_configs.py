@@ -148,6 +148,11 @@ def bench_models(args, dist, rank, world):
         gbs = bpp * n / (kern_ms * 1e-3) / 1e9
         per[name] = {"pairs_per_s": n * world * args.steps * reps / elapsed, "kernel_ms": kern_ms, "GB_s": gbs,
                      "roofline_frac": gbs / HBM_PEAK_GBS, "bytes_per_pair": bpp}
+        if name == "Merl":
+            # the table entry each pair reads is algorithmic data too (one float4 of the 23 MB table; random
+            # directions touch a different cache line per pair, which the Infinity Cache serves)
+            per[name]["with_table_gather"] = {"bytes_per_pair": 52,
+                                              "roofline_frac": 52 * n / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         vr = valu_roofline(f"models:{name}", kern_ms, n)
         if vr["frac"] is not None:
             # VALU-bound models: the fraction of the chip's VALU issue slots, from committed counters of this kernel
