@@ -114,6 +114,13 @@ struct FresnelComplexRGB
   {
     for (int c = 0; c < 3; ++c) { n[c] = q[c]; k[c] = q[3 + c]; }
   }
+  // With VALUE = Spectrum (he.h:116, 490-496) every operation is the native backbone's array arithmetic in float:
+  // a double scalar on the left of an array (0.5 * (a2b2 + temp), 0.5 * (Rs + Rp)) converts to float first
+  // (array.h:95, friend operator*(const T&, array)), and Rs / Rp are Spectrum -- so the reference's float at every
+  // step, IEEE float quotients (div_nr: the correctly rounded quotient, with the IEEE fallback off the normal range)
+  // and correctly rounded square roots (safe_sqrtf).  (Rounds 1-4 evaluated the numerators and denominators in
+  // double, as the scalar-VALUE instantiation does (EPD's FresnelComplex, epd.hpp): the He family's backscatter values
+  // were then 1-10 ulp off on 80-100 % of the 90 sampler-CDF directions, profiles/r05_he_cdf_before.json.)
   __device__ __forceinline__ void eval3(float cs, float* F) const
   {
     const float c2 = cs * cs;
@@ -122,16 +129,14 @@ struct FresnelComplexRGB
     for (int c = 0; c < 3; ++c)
     {
       const float n2 = n[c] * n[c], k2 = k[c] * k[c];
-      const float temp = n2 - k2 - s2;
-      const float a2b2 = safe_sqrtf(temp * temp + 4 * n2 * k2);
-      const double a = safe_sqrt(0.5 * double(a2b2 + temp));
-      const double a2c = 2 * a * double(cs);
-      // numerators and denominators in double like the reference (they cancel near n = 1); the quotients
-      // only need float accuracy: F = float(0.5 (Rs + Rp)) of two positive terms
-      const float Rs = f_div_d(double(a2b2) - a2c + double(c2), double(a2b2) + a2c + double(c2));
-      const double ca = double(c2 * a2b2);
-      const float Rp = f_div_d(double(Rs) * (ca - (a2c - double(s2)) * double(s2)), ca + (a2c + double(s2)) * double(s2));
-      F[c] = float(0.5 * (double(Rs) + double(Rp)));
+      const float temp = (n2 - k2) - s2;
+      const float a2b2 = safe_sqrtf(temp * temp + (n2 * 4.0f) * k2);
+      const float a = safe_sqrtf((a2b2 + temp) * 0.5f);
+      const float a2c = (a * 2.0f) * cs;
+      const float Rs = div_nr((a2b2 - a2c) + c2, (a2b2 + a2c) + c2);
+      const float ca = c2 * a2b2;
+      const float Rp = div_nr(Rs * (ca - (a2c - s2) * s2), ca + (a2c + s2) * s2);
+      F[c] = (Rs + Rp) * 0.5f;
     }
   }
 };
