@@ -5,3 +5,5 @@ timeout -k 10 700 python -u -m pytest -q --timeout 300 --timeout-method thread t
 mkdir -p gpurun_out/parity_n && cp gpurun_out/parity_*.json gpurun_out/parity_n/
 export AB_ARGS="--workload models --models He,HeWestin,HeHolzschuch,NganHe --steps 10 --warmup 2 --no-cpu"
 bash tools/gpu_step.sh ab:he2,2,base,hetab || exit 1
+export AB_ARGS="--workload models --models EPD --steps 20 --warmup 3 --no-cpu"
+bash tools/gpu_step.sh ab:epd1,2,base,epdtab || exit 1
