@@ -58,11 +58,7 @@ __device__ __forceinline__ float epd_g1_lookup(const float* tab, float p, float 
   const double L = (it == 0.0f) ? -__builtin_inf() : ((it > 3.40282347e38f) ? __builtin_inf()
                    : ((it != it) ? double(it) : double(float(log2_acc(it) * 0.69314718055994530942))));
 #endif
-#ifdef BBM_HIP_EPD_EXP_TAB      // A/B: the LDS-table double exponential (math.hpp exp_dd_t)
-  const double e1 = __builtin_isfinite(L) ? exp_dd_t(-exp_dd_t(L * 0.05)) : ((L > 0.0) ? 0.0 : 1.0);
-#else
   const double e1 = __builtin_isfinite(L) ? exp_dd(-exp_dd(L * 0.05)) : ((L > 0.0) ? 0.0 : 1.0);
-#endif
   const double m1 = (L != L) ? L : e1 * 1000.0 - 1.0;        // NaN stays NaN
 #endif
   auto at = [&](double i0, double i1) {

@@ -97,16 +97,6 @@ __device__ __forceinline__ v3 ndf_sampler_halfway(const float* __restrict__ cdf,
   return sph_to_vec(phi, theta);
 }
 
-// the series' double exponential: exp_dd (a 9-FMA polynomial); -DBBM_HIP_HE_EXP_TAB (A/B): exp_dd_t (LDS table)
-__device__ __forceinline__ double he_exp(double a)
-{
-#ifdef BBM_HIP_HE_EXP_TAB
-  return exp_dd_t(a);
-#else
-  return exp_dd(a);
-#endif
-}
-
 // ln x for the early-exit bound: exact exponent (frexp, subnormals included) + v_log_f32 of the mantissa, ~1e-7
 // absolute; -inf for 0 (a zero gm or g makes every later term 0)
 __device__ __forceinline__ float ln_bound(float x)
@@ -347,7 +337,7 @@ struct He
 #pragma unroll
     for (int c = 0; c < 3; ++c)
     {
-      eg[c] = converged ? 0.0 : he_exp(-g[c]);
+      eg[c] = converged ? 0.0 : exp_dd(-g[c]);
       lng[c] = (ADAPTIVE && WESTIN) ? ln_bound(float(g[c])) : 0.0f;
       cap[c] = eg[c] * eb64;
     }
@@ -383,9 +373,9 @@ struct He
       if (WESTIN)
       {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) ex[c] = he_exp(-double(div_small(eb[c], mf, rmf)));
+        for (int c = 0; c < 3; ++c) ex[c] = exp_dd(-double(div_small(eb[c], mf, rmf)));
       }
-      else ex[0] = ex[1] = ex[2] = he_exp(-double(div_small(eb[0], mf, rmf)));   // eb is the same for every channel
+      else ex[0] = ex[1] = ex[2] = exp_dd(-double(div_small(eb[0], mf, rmf)));   // eb is the same for every channel
 #pragma unroll
       for (int c = 0; c < 3; ++c)
       {

@@ -484,7 +484,7 @@ struct LowSmooth
   }
   __device__ __forceinline__ static double pow2d(double x) { return x * x; }
 
-  // exact mode (bbm_hip_set_exact_subnormals): S's double power computed in double (f64::pow_d), rounded to float
+  // S's double power computed in double (f64::pow_d), rounded to float, in every mode (exact mode: the same)
   static constexpr bool kHasExact = true;
   template<int MODE, bool EXACT = false>
   __device__ __forceinline__ void eval_pdf(v3 in, v3 out, uint32_t component, float* rgb, float& pdf) const
@@ -494,9 +494,8 @@ struct LowSmooth
     {
       const float dp2 = sqnorm2(in.x + out.x, in.y + out.y);
       const float cosD = float(safe_sqrt(1 - 0.25 * sqnorm2(in.x - out.x, in.y - out.y)));
-      float S;                                                  // double pow in the reference; see LowNdf::eval
-      if constexpr (EXACT) S = float(f64::pow_d(1.0 + double(B * dp2), -double(C)));   // B Dp2 is a float product
-      else S = powf_fast(float(1.0 + B * dp2), -C);
+      // the reference's double pow; round 5: in every mode (+1.3 % kernel time, profiles/r05_ab_low_exact.txt)
+      const float S = float(f64::pow_d(1.0 + double(B * dp2), -double(C)));   // B Dp2 is a float product
       const float Q = fres.eval(cosD);
 #pragma unroll
       for (int c = 0; c < 3; ++c) rgb[c] = active ? A[c] * S * Q : 0.0f;

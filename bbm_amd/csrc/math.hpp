@@ -501,27 +501,6 @@ __device__ __forceinline__ float powf_glibc(float x, float y)
   return (y == 0.0f || x == 1.0f) ? 1.0f : res;
 }
 
-// e^a in double as exp_dd (~2^-44 relative, the same argument rounding) from glibc's 2^(j/32) table (the kernel's LDS
-// copy) and a degree-5 polynomial in the remainder r (|r| <= 1/2 in units of ln2 / 32): 5 FMAs instead of exp_dd's 9,
-// and a shorter dependent chain; ldexp applies the exponent, subnormal and zero results included
-template<bool LDS = true>
-__device__ __forceinline__ double exp_dd_t(double a)
-{
-  const double z = a * 0x1.71547652b82fep+5;                      // 32 / ln 2
-  constexpr double kShift = 0x1.8p+52;
-  const double kb = z + kShift;
-  const uint32_t ki = uint32_t(__builtin_bit_cast(uint64_t, kb));
-  const double r = z - (kb - kShift);
-  double p = __builtin_fma(0x1.5d87fe78a6731p-35, r, 0x1.3b2ab6fba4e77p-27);
-  p = __builtin_fma(p, r, 0x1.c6b08d704a0c0p-20);
-  p = __builtin_fma(p, r, 0x1.ebfbdff82c58fp-13);
-  p = __builtin_fma(p, r, 0x1.62e42fefa39efp-6);
-  p = __builtin_fma(p, r, 1.0);
-  const uint32_t j = ki & 31u;
-  const double s = __builtin_bit_cast(double, expf_tab<LDS>(j) + (uint64_t(j) << 47));   // 2^(j/32)
-  return __builtin_ldexp(p * s, int32_t(ki) >> 5);
-}
-
 // powf_glibc for a finite normal x > 0 and a finite y: the same steps without the special-operand selects and the
 // subnormal normalisation (pow(1, y) and pow(x, 0) come out as exactly 1 from the table row {1, 0} and r = 0), for the
 // sites whose base is provably a positive normal float (Bagher's t = alpha + tan^2 / alpha, alpha >= its lower bound)

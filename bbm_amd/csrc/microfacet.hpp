@@ -403,6 +403,14 @@ struct HeightCorrelated
   }
 };
 
+// The Low NDF's double power in every mode (A/B: -DBBM_HIP_LOW_EXACT_DEFAULT); by default powf_fast (~1e-6) outside
+// exact mode: the double power cost LowMicrofacet(Fit) +8.5 % per 10 M pairs (profiles/r05_ab_low_exact.txt)
+#ifdef BBM_HIP_LOW_EXACT_DEFAULT
+constexpr bool kLowExactDefault = true;
+#else
+constexpr bool kLowExactDefault = false;
+#endif
+
 // ndf::low (include/ndf/low.h:32-141): the unnormalised ABC "S" term of [Low 2012] as an NDF.
 // eval pow(1 + B (1 - z), -C) in double; pdf = eval B (1/(2 pi)) normalization with the
 // normalization a per-thread double constant; sample inverts the marginal CDF of cos(theta)
@@ -429,7 +437,7 @@ struct LowNdf
     // pow(1 + B (1 - z), -C) in double in the reference; powf_fast: within ~1e-6; EXACT (exact mode): the double
     // power (f64::pow_d) of the double base, rounded to float
     float S;
-    if constexpr (EXACT) S = float(f64::pow_d(1.0 + double(B) * (1.0 - double(h.z)), -double(C)));
+    if constexpr (EXACT || kLowExactDefault) S = float(f64::pow_d(1.0 + double(B) * (1.0 - double(h.z)), -double(C)));
     else S = powf_fast(float(1.0 + B * (1.0 - h.z)), -C);
     return (h.z > 0) ? S : 0.0f;
   }
