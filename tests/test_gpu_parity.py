@@ -34,7 +34,11 @@ META = ou.golden_meta()
 INP = ou.golden_inputs()
 TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
 MAX_EXCUSED_FRAC = 1e-3       # at most this fraction of a batch's lanes may need an input-ulps proof
-MAX_SAMPLER_FRAC = 0.05       # ... a sampler-CDF proof (a CDF entry moves the ~2/90 of directions in its bins)
+# ... a sampler-CDF proof (a CDF entry moves the ~2/90 of directions in its bins).  Round 5: none may -- the He family's
+# 90 backscatter evaluations behind the CDF follow the reference's float complex Fresnel (he.hpp FresnelComplexRGB),
+# so the GPU's CDF is the reference's and no lane of any golden set or 1 M batch needed this proof (r05_parity_*.json;
+# round 4: 6 509 eval/pdf and 1 279 sampling lanes per 1 M for HeWestin).  The prover stays as the diagnostic.
+MAX_SAMPLER_FRAC = 0.0
 # Ceiling on the relative error of the lanes that pass by a proof (the proofs bound WHY a lane differs, this bounds
 # HOW MUCH).  History: round 3 Bagher / Aggregate(Lambertian, Bagher) 5e-2 and the He family 2e-2 (the ill-conditioned
 # lanes of Bagher's shadowing 1 + Lambda (1 - e^(c t^k)) and of He's series at tiny D); round 4 (glibc powf / expf /
@@ -105,7 +109,7 @@ def check_lanes(got, ref, what, provers=(), model=None):
     n_sampler = proven.get("sampler_cdf", 0)
     assert bad.size - n_sampler <= max(2, MAX_EXCUSED_FRAC * n), \
         f"{what}: {bad.size - n_sampler} of {n} lanes needed an input-ulps proof ({proven})"
-    assert n_sampler <= max(2, MAX_SAMPLER_FRAC * n), f"{what}: {n_sampler} of {n} lanes needed a sampler-CDF proof"
+    assert n_sampler <= MAX_SAMPLER_FRAC * n, f"{what}: {n_sampler} of {n} lanes needed a sampler-CDF proof"
     gb, rb = got[..., bad], ref[..., bad]
     big = np.abs(rb) >= TINY
     excused = ou.max_rel_normal(np.where(big, gb, rb), rb) if bad.size else 0.0
