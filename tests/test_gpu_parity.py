@@ -36,7 +36,7 @@ TABULATED_SAMPLERS = {"He", "HeWestin", "HeHolzschuch", "NganHe"}
 MAX_EXCUSED_FRAC = 1e-3       # at most this fraction of a batch's lanes may need an input-ulps proof
 # ... a sampler-CDF proof (a CDF entry moves the ~2/90 of directions in its bins).  Round 5: none may -- the He family's
 # 90 backscatter evaluations behind the CDF follow the reference's float complex Fresnel (he.hpp FresnelComplexRGB),
-# so the GPU's CDF is the reference's and no lane of any golden set or 1 M batch needed this proof (r05_parity_*.json;
+# within 1-4 ulp where not bit-identical, and no lane of any golden set or 1 M batch needed this proof (r05_parity_*.json;
 # round 4: 6 509 eval/pdf and 1 279 sampling lanes per 1 M for HeWestin).  The prover stays as the diagnostic.
 MAX_SAMPLER_FRAC = 0.0
 # Ceiling on the relative error of the lanes that pass by a proof (the proofs bound WHY a lane differs, this bounds
