@@ -140,6 +140,12 @@ template<class Model> struct eval_prefetch { static constexpr bool value = false
 template<class Model> struct eval_prefetch { static constexpr bool value = true; };
 #endif
 
+// Whether a model's evaluation reads the glibc tables (math.hpp expf / logf / powf and what is built on them): the
+// eval kernel skips the LDS prologue for the models declared table-free (models.hpp: Lambertian, GGX, GGXHeitz and
+// their aggregate), which paid 3-4 % for it (profiles/r05_ab_lds_tables.txt).  Checked by a poisoned build
+// (-DBBM_HIP_TABLES_POISON: NaN tables instead of none) under the parity tests.
+template<class Model> struct uses_math_tables { static constexpr bool value = true; };
+
 // Software pipelining of k_eval_pdf_v4's grid-stride loop: the next quad's six loads are issued before the current
 // quad is evaluated, so a thread's HBM latency hides under its own compute (with a capped grid, eval_grid_cap, every
 // thread runs several iterations).  For the latency-bound models whose waves otherwise all wait on their loads at
@@ -170,7 +176,10 @@ void k_eval_pdf_v4(EvalArgs a)
   constexpr bool pipe = eval_pipeline<Model>::value;
   constexpr bool pf = eval_prefetch<Model>::value || pipe;
   if (pf && t < n4) load(t);
-  math_tables_init();
+  if constexpr (uses_math_tables<Model>::value) math_tables_init();
+#ifdef BBM_HIP_TABLES_POISON
+  else math_tables_poison();
+#endif
   const Model m(a.p.v);
   for (bool first = true; t < n4; t += stride, first = false)
   {

@@ -422,6 +422,24 @@ __device__ __forceinline__ double logf_tab(uint32_t i, int c)
 // Every kernel's first statement (tests/test_kernel_prologue.py checks that every kernel of the library starts with
 // it): lanes 0..31 of every wave fill the tables; the wave's later reads of them follow in program order (a
 // wavefront-scope fence keeps the compiler from moving them above the stores)
+// Validation builds only (-DBBM_HIP_TABLES_POISON): what a kernel whose model is declared table-free
+// (uses_math_tables, kernels.hpp) writes instead of the tables -- NaN everywhere, so any lookup shows in the parity
+// tests.
+__device__ __forceinline__ void math_tables_poison()
+{
+#ifndef BBM_HIP_CONST_TABLES
+  const unsigned t = threadIdx.x & 63u;
+  if (t < 32)
+  {
+    g_lds_exptab[t] = 0x7ff8000000000000ull;
+    g_lds_logftab[t >> 1][t & 1] = __builtin_nan("");
+    g_lds_log2tab[t >> 1][t & 1] = __builtin_nan("");
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 __device__ __forceinline__ void math_tables_init()
 {
 #ifndef BBM_HIP_CONST_TABLES

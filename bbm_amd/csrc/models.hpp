@@ -73,6 +73,10 @@ using CookTorranceWalterM = Microfacet<Beckmann<false, true>, Uncorrelated, Fres
 
 using CookTorranceHeitzM = Microfacet<Beckmann<true, true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;   // bsdfmodel/cooktorranceheitz.h:33-39
 using GGXHeitzM = Microfacet<GGX<true>, HeightCorrelated, FresnelCook, Norm::Walter, true>;                     // bsdfmodel/ggxheitz.h:28-34
+// eval reads no glibc table (GGX's D, G1 and FresnelCook are rational / sqrt; Lambertian is a constant)
+template<> struct uses_math_tables<Lambertian> { static constexpr bool value = false; };
+template<> struct uses_math_tables<GGXM> { static constexpr bool value = false; };
+template<> struct uses_math_tables<GGXHeitzM> { static constexpr bool value = false; };
 using NganCookTorranceM = Microfacet<Beckmann<false, true>, VGroove, FresnelSchlick, Norm::Cook, true>;         // bsdfmodel/ngan.h:141-147
 using PhongWalterM = Microfacet<PhongNdf, Uncorrelated, FresnelCook, Norm::Walter, true>;                         // bsdfmodel/phongwalter.h:27-33
 #ifdef BBM_HIP_MIDTIER_WAVES   // A/B: the mid-tier microfacet variants' occupancy
@@ -115,6 +119,7 @@ using NganASM = AshikhminShirley<ScalarFresnel3<FresnelSchlick>, false, true, fa
 using AggBagherM = Aggregate<Lambertian, Bagher>;
 using AggCookTorranceM = Aggregate<Lambertian, CookTorranceM>;
 using AggGGXM = Aggregate<Lambertian, GGXM>;
+template<> struct uses_math_tables<AggGGXM> { static constexpr bool value = false; };
 using AggLowASM = Aggregate<Lambertian, LowASM>;
 using AggLowMicrofacetM = Aggregate<Lambertian, LowMicrofacetM>;
 using AggLowSmoothM = Aggregate<Lambertian, LowSmooth>;
