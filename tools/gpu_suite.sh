@@ -1,3 +1,4 @@
+# Full GPU verification: the C++ adapter check against the reference, then every -m gpu test (records under gpurun_out/).
 set -o pipefail
 timeout -k 10 300 tests/cpp/_build/adapter_check > gpurun_out/adapter_m.jsonl 2> gpurun_out/adapter_m.err; echo adapter rc=$?
 grep -c '"ok": false' gpurun_out/adapter_m.jsonl
