@@ -92,7 +92,9 @@ SIGNATURES = {
     "bbm_hip_allreduce_sums": (_I, [_P, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
+CALL_EXACT = 0x20000000     # BBM_HIP_CALL_EXACT: OR-ed into a model id, this call in exact mode
+CALL_DEFAULT = 0x10000000   # BBM_HIP_CALL_DEFAULT: this call in default mode (whatever set_exact_subnormals says)
 AGGREGATE = -100        # BBM_HIP_AGGREGATE: model id of a composed-aggregate node (bbm_hip_child.children)
 AGGREGATE_BSDF = -101   # BBM_HIP_AGGREGATE_BSDF: a composed runtime aggregate (aggregatebsdf, what fromString builds)
 RUNTIME_AGGREGATE = 0x40000000   # BBM_HIP_RUNTIME_AGGREGATE: OR-ed into a fused aggregate's id -> aggregatebsdf semantics
@@ -114,7 +116,7 @@ class ChildF64(ctypes.Structure):
 class Rng(ctypes.Structure):
     """bbm_hip_rng (include/bbm_hip.h): the state of bbm::rng<Size_t> (std::mt19937_64 + uniform_int_distribution)."""
     _fields_ = [("mt", ctypes.c_uint64 * 312), ("pos", ctypes.c_uint64), ("lower", ctypes.c_uint64),
-                ("upper", ctypes.c_uint64)]
+                ("upper", ctypes.c_uint64), ("magic", ctypes.c_uint64)]
 
 
 COMM_ID_BYTES = 128     # BBM_HIP_COMM_ID_BYTES

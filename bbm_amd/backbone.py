@@ -270,6 +270,13 @@ class BsdfModel:
     __repr__ = __str__
 
     # ---------------------------------------------------------------- batched evaluation
+    def _call_id(self, exact):
+        """The model id for one call: exact=None follows set_exact_subnormals (the process-wide default), True / False
+        force exact / default mode for this call only (BBM_HIP_CALL_EXACT / BBM_HIP_CALL_DEFAULT, re-entrant)."""
+        if exact is None:
+            return self.model_id
+        return self.model_id | (_lib.CALL_EXACT if exact else _lib.CALL_DEFAULT)
+
     def _pptr(self):
         return self._params.ctypes.data_as(ctypes.c_void_p)
 
@@ -304,7 +311,7 @@ class BsdfModel:
         return rgb, pdf
 
     def eval_pdf(self, in_, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *,
-                 rgb=None, pdf=None, stream=None, mode=3, params64=None):
+                 rgb=None, pdf=None, stream=None, mode=3, params64=None, exact=None):
         torch = _torch()
         if _is_f64(in_):
             rgb, pdf = self._eval_pdf_f64(in_, out, component, unit, mask, rgb if mode & 1 else None,
@@ -323,15 +330,16 @@ class BsdfModel:
         lib = _lib.load()
         s = _stream_ptr(stream)
         _on_stream(stream, _keep, rgb, pdf)
+        mid = self._call_id(exact)
         if mode == 3:
-            rc = lib.bbm_hip_eval_pdf(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+            rc = lib.bbm_hip_eval_pdf(mid, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
                                       int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),
                                       rgb[2].data_ptr(), pdf.data_ptr(), s)
         elif mode == 1:
-            rc = lib.bbm_hip_eval(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+            rc = lib.bbm_hip_eval(mid, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
                                   int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(), rgb[2].data_ptr(), s)
         else:
-            rc = lib.bbm_hip_pdf(self.model_id, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
+            rc = lib.bbm_hip_pdf(mid, self._pptr(), self._params.size, ix, iy, iz, ox, oy, oz, mptr, n,
                                  int(component), int(unit), pdf.data_ptr(), s)
         _lib.check(rc)
         return rgb, pdf
@@ -345,9 +353,9 @@ class BsdfModel:
         return self.eval_pdf(in_, out, component, unit, mask, mode=2, **kw)[1]
 
     def sample(self, out, xi, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None,
-               params64=None):
+               params64=None, exact=None):
         """BsdfSample sample(out, xi, component, unit, mask) for N (out, xi) -> BsdfSample (float64 out / xi: the
-        doubleRGB kernels, float64 direction and pdf)."""
+        doubleRGB kernels, float64 direction and pdf).  exact: as eval_pdf."""
         torch = _torch()
         f64 = _is_f64(out)
         dt = torch.float64 if f64 else torch.float32
@@ -373,13 +381,13 @@ class BsdfModel:
             fn, pp, npar = lib.bbm_hip_sample_f64, prm.ctypes.data_as(ctypes.c_void_p), prm.size
         else:
             fn, pp, npar = lib.bbm_hip_sample, self._pptr(), self._params.size
-        _lib.check(fn(self.model_id, pp, npar, ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
+        _lib.check(fn(self._call_id(exact), pp, npar, ox, oy, oz, x0.data_ptr(), x1.data_ptr(), mptr, n, int(component),
                       int(unit), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), p.data_ptr(), f.data_ptr(),
                       _stream_ptr(stream)))
         return BsdfSample(d, p, f)
 
     def reflectance(self, out, component=bsdf_flag.All, unit=unit_t.Radiance, mask=None, *, stream=None,
-                    params64=None):
+                    params64=None, exact=None):
         """Spectrum reflectance(out, component, unit, mask) for N directions -> (3, N) RGB (float64 directions:
         the doubleRGB kernels, float64 RGB)."""
         torch = _torch()
@@ -400,7 +408,7 @@ class BsdfModel:
         rgb = torch.empty((3, n), dtype=torch.float32, device=dev)
         _on_stream(stream, _keep, rgb)
         lib = _lib.load()
-        _lib.check(lib.bbm_hip_reflectance(self.model_id, self._pptr(), self._params.size, ox, oy, oz, mptr, n,
+        _lib.check(lib.bbm_hip_reflectance(self._call_id(exact), self._pptr(), self._params.size, ox, oy, oz, mptr, n,
                                            int(component), int(unit), rgb[0].data_ptr(), rgb[1].data_ptr(),
                                            rgb[2].data_ptr(), _stream_ptr(stream)))
         return rgb

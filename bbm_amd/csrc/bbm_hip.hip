@@ -410,7 +410,7 @@ int num_models() { return int(registry().models.size()); }
 bool runtime_id(int id) { return id >= 0 && (id & BBM_HIP_RUNTIME_AGGREGATE) != 0; }
 const ModelEntry* entry(int id)
 {
-  const int base = (id >= 0) ? (id & ~BBM_HIP_RUNTIME_AGGREGATE) : id;
+  const int base = (id >= 0) ? (id & ~(BBM_HIP_RUNTIME_AGGREGATE | BBM_HIP_CALL_EXACT | BBM_HIP_CALL_DEFAULT)) : id;
   if (base < 0 || base >= num_models()) return nullptr;
   const ModelEntry* e = &registry().models[size_t(base)];
   if (runtime_id(id) && base < kNumSingle) return nullptr;    // the flag applies to fused aggregates only
@@ -677,6 +677,7 @@ static int eval_common(int mode, int model_id, const float* params, int nparams,
                        float* r, float* g, float* b, float* pdf, void* stream)
 {
   (void)unit;   // no model on this path depends on unit_t (bsdfmodel/microfacet.h:74, lambertian.h:45)
+  const CallExactScope mode_scope(model_id);
   EvalArgs a;
   const ModelEntry* e;
   int rc = prepare(model_id, params, nparams, n, a, e);
@@ -729,6 +730,7 @@ int bbm_hip_sample(int model_id, const float* params, int nparams,
                    void* stream)
 {
   (void)unit;
+  const CallExactScope mode_scope(model_id);
   EvalArgs tmp;
   const ModelEntry* e;
   int rc = prepare(model_id, params, nparams, n, tmp, e);
@@ -753,6 +755,7 @@ int bbm_hip_reflectance(int model_id, const float* params, int nparams,
                         float* r, float* g, float* b, void* stream)
 {
   (void)unit;
+  const CallExactScope mode_scope(model_id);
   EvalArgs tmp;
   const ModelEntry* e;
   int rc = prepare(model_id, params, nparams, n, tmp, e);
@@ -1011,6 +1014,7 @@ size_t bbm_hip_check_workspace_size(const bbm_hip_check_desc* d)
 int bbm_hip_check(int model_id, const float* params, int nparams, const bbm_hip_check_desc* d,
                   double* acc, uint64_t* counts, void* workspace, size_t workspace_bytes, void* stream)
 {
+  const CallExactScope mode_scope(model_id);
   const ModelEntry* e = entry(model_id);
   if (!e) return fail(BBM_HIP_ERR_INVALID_MODEL, "unknown model id " + std::to_string(model_id));
   if (nparams != e->nparams)

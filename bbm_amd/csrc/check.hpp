@@ -324,7 +324,7 @@ int launch_check(int test, const CheckArgs& a0, double* acc, hipStream_t s)
   const dim3 grid(bx, unsigned(a.nslots));
   bool launched = false;
   if constexpr (has_exact_sample<Model>())       // exact mode: the sampler's twin with glibc's erff / logf (math.hpp)
-    if (exact_subnormals().load() != 0) launched = launch_check_kernel<exact_sample_t<Model>, true>(test, grid, a, s);
+    if (exact_on()) launched = launch_check_kernel<exact_sample_t<Model>, true>(test, grid, a, s);
   if (!launched && !launch_check_kernel<Model, false>(test, grid, a, s))
     return fail(BBM_HIP_ERR_INVALID_ARG, "unknown check test");
   if (test != kCheckSampleCount)

@@ -10,7 +10,8 @@
 // The p- and r-independent pieces (the q_i, dq_i of the P2 loop, the r_j, dr_j, t_j of the series, N per
 // row) are evaluated on the host with the C library's float/double functions and the generator's exact
 // float/double expression types; the 100 x 999 P2 integrals (1e9 terms) run on the GPU, one thread per
-// (row, j) summing its 10 000 terms serially in float like the generator; the recurrence, G1 = 1/(1+Delta)
+// (row, j) summing its 10 000 terms serially in float like the generator (with the generator build's FMA
+// contractions); the recurrence, G1 = 1/(1+Delta)
 // and the rounding to 6 significant digits (the generator prints with bbm::toString, i.e. ostream <<
 // float) are host work again.  Built once per device, on first use of an EPD model.
 #include <cmath>
@@ -44,8 +45,9 @@ __global__ __launch_bounds__(256) void k_epd_p2(const float* __restrict__ dq, co
   {
     const float qi = q[i];
     // glibc's expf / powf, what the generator called (G1.cpp:91-223 on x86-64), restated bit for bit (math.hpp):
-    // the device's ~1-ulp f32 versions, or even the correctly rounded floats, would perturb the summation
-    integral += dq[i] * expf_glibc(-powf_glibc(r2 + qi * qi, p));
+    // the device's ~1-ulp f32 versions, or even the correctly rounded floats, would perturb the summation.  The two
+    // multiply-adds are FMAs, as in the build that produced the shipped G1.h (see build_table)
+    integral = __builtin_fmaf(dq[i], expf_glibc(-powf_glibc(__builtin_fmaf(qi, qi, r2), p)), integral);
   }
   out[row * kEpdCols + j] = float(2.0 * double(norm[row]) * double(integral));
 }
@@ -120,7 +122,12 @@ int build_table(hipStream_t s, EpdTable& t)
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "synchronize");
   for (float* d : {d_dq, d_q, d_r, d_p, d_n, d_out}) (void)hipFree(d);
 
-  // the Delta recurrence and G1 = 1 / (1 + Delta) per row (G1.cpp:186-220), then the 6-digit print
+  // the Delta recurrence and G1 = 1 / (1 + Delta) per row (G1.cpp:186-220), then the 6-digit print.  The shipped
+  // G1.h is the output of a build with FMA contraction (gnu++20's default -ffp-contract=fast with FMA available):
+  // G1.cpp compiled so here prints it byte for byte in every entry, and its code has exactly three vfmadd -- P2's
+  // r2 + q*q and integral += dq * exp(...) (k_epd_p2) and the series' integral[j] += (r t - 1) p2 below.  Each op
+  // rounded on its own instead, 3.6 % of the entries differ in the 6th digit (tests/test_oracle.py::
+  // test_epd_g1_generator_recipe pins the recipe on the CPU, test_gpu_parity.py the table built here).
   t.host.assign(size_t(kEpdRows) * kEpdCols, 0.0f);
   for (int r = 0; r < kEpdRows; ++r)
   {
@@ -134,7 +141,7 @@ int build_table(hipStream_t s, EpdTable& t)
         const float p2j = p2[size_t(r) * kEpdCols + j] * dr[j];
         float v = 0.0f;
         if (prev > 0) v = (integral[j - 1] + Pj) * tt / prev - Pj;
-        if (rj[j] * tt > 1) v += (rj[j] * tt - 1) * p2j;
+        if (rj[j] * tt > 1) v = std::fma(rj[j] * tt - 1, p2j, v);
         integral[j] = v;
         prev = tt;
         Pj += p2j;

@@ -82,7 +82,25 @@ inline std::atomic<int>& exact_subnormals()
   return v;
 }
 
-template<class Model> inline bool exact_launch() { return model_has_exact<Model>() && exact_subnormals().load() != 0; }
+// per-call override (BBM_HIP_CALL_EXACT / BBM_HIP_CALL_DEFAULT OR-ed into a model id): -1 = follow the process-wide
+// switch.  Thread-local and scoped to the entry point that decoded the id (CallExactScope), so concurrent calls
+// from different threads never see each other's mode; the launches are enqueued on the calling thread.
+inline thread_local int t_call_exact = -1;
+inline bool exact_on() { return t_call_exact >= 0 ? t_call_exact != 0 : exact_subnormals().load() != 0; }
+struct CallExactScope
+{
+  int prev;
+  explicit CallExactScope(int id) : prev(t_call_exact)
+  {
+    if (id >= 0 && (id & BBM_HIP_CALL_EXACT)) t_call_exact = 1;
+    else if (id >= 0 && (id & BBM_HIP_CALL_DEFAULT)) t_call_exact = 0;
+  }
+  ~CallExactScope() { t_call_exact = prev; }
+  CallExactScope(const CallExactScope&) = delete;
+  CallExactScope& operator=(const CallExactScope&) = delete;
+};
+
+template<class Model> inline bool exact_launch() { return model_has_exact<Model>() && exact_on(); }
 
 template<class Model, int MODE, bool EXACT = false>
 __device__ __forceinline__ void one_pair(const Model& m, const EvalArgs& a, uint64_t i, bool active)
@@ -750,7 +768,7 @@ int launch_sample_mask(const SampleArgs& a0, hipStream_t s)
   if (blocks > max_blocks()) blocks = max_blocks();
   bool twin = false;
   if constexpr (has_exact_sample<Model>())       // exact mode: the sampler's twin with glibc's erff / logf (math.hpp)
-    if (exact_subnormals().load() != 0)
+    if (exact_on())
     {
       using T = exact_sample_t<Model>;
       if (vec) hipLaunchKernelGGL((k_sample_v4<T, MASK>), dim3(unsigned(blocks)), dim3(kBlock), 0, s, a);

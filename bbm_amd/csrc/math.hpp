@@ -420,16 +420,16 @@ __device__ __forceinline__ double logf_tab(uint32_t i, int c)
   return kLogfTab[i][c];
 }
 // Every kernel's first statement (tests/test_kernel_prologue.py checks that every kernel of the library starts with
-// it): lanes 0..31 of every wave fill the tables; the wave's later reads of them follow in program order (a
-// wavefront-scope fence keeps the compiler from moving them above the stores)
+// it): every wave fills the tables with its active lanes (below); the wave's later reads of them follow in program
+// order (a wavefront-scope fence keeps the compiler from moving them above the stores)
 // Validation builds only (-DBBM_HIP_TABLES_POISON): what a kernel whose model is declared table-free
 // (uses_math_tables, kernels.hpp) writes instead of the tables -- NaN everywhere, so any lookup shows in the parity
 // tests.
 __device__ __forceinline__ void math_tables_poison()
 {
 #ifndef BBM_HIP_CONST_TABLES
-  const unsigned t = threadIdx.x & 63u;
-  if (t < 32)
+  const unsigned nl = unsigned(__builtin_popcountll(__builtin_amdgcn_read_exec()));
+  for (unsigned t = __lane_id(); t < 32; t += nl)
   {
     g_lds_exptab[t] = 0x7ff8000000000000ull;
     g_lds_logftab[t >> 1][t & 1] = __builtin_nan("");
@@ -443,8 +443,11 @@ __device__ __forceinline__ void math_tables_poison()
 __device__ __forceinline__ void math_tables_init()
 {
 #ifndef BBM_HIP_CONST_TABLES
-  const unsigned t = threadIdx.x & 63u;
-  if (t < 32)
+  // each wave writes the 32 entries it will read itself (no workgroup barrier): the wave's active lanes -- all 64, or
+  // the low lanes of a partial wave (a block smaller than a wave, a ragged last wave, any block shape) -- stride over
+  // the entries, so every entry is written whatever the wave's population
+  const unsigned nl = unsigned(__builtin_popcountll(__builtin_amdgcn_read_exec()));
+  for (unsigned t = __lane_id(); t < 32; t += nl)
   {
     g_lds_exptab[t] = kExpfTab[t];
     g_lds_logftab[t >> 1][t & 1] = kLogfTab[t >> 1][t & 1];
@@ -550,6 +553,24 @@ __device__ __forceinline__ float powf_glibc_pos(float x, float y)
   float res = float(e * s);
   res = (ylogx > 0x1.fffffffd1d571p+6) ? __builtin_inff() : res;
   return (ylogx <= -150.0) ? 0.0f : res;
+}
+
+// glibc's powf over every operand, negative bases included (e_powf.c: checkint -- an integer y gives |x|^y with the
+// sign of x for odd y, a non-integer y NaN; -0 and -inf as +0 / +inf except for odd integers; pow(-1, +-inf) = 1):
+// for parameters outside an attribute's range (Bagher's D with alpha <= 0, spectral.hpp), never on a hot path
+template<bool LDS = true>
+__device__ __forceinline__ float powf_glibc_any(float x, float y)
+{
+  if (!__builtin_signbit(x) || x != x) return powf_glibc<LDS>(x, y);
+  const float ax = __builtin_fabsf(x);
+  if (y == 0.0f) return 1.0f;
+  if (y != y) return y;
+  if (__builtin_isinf(y)) return (ax == 1.0f) ? 1.0f : powf_glibc<LDS>(ax, y);
+  const bool integer = __builtin_truncf(y) == y;
+  if (!integer) return (ax == 0.0f || __builtin_isinf(ax)) ? powf_glibc<LDS>(ax, y) : __builtin_nanf("");
+  const bool odd = __builtin_fabsf(y) < 0x1p24f && (int32_t(y) & 1) != 0;
+  const float r = powf_glibc<LDS>(ax, y);
+  return odd ? -r : r;
 }
 
 // glibc 2.35's erff / erfcf (sysdeps/ieee754/flt-32/s_erff.c: Sun fdlibm's rational approximations in float

@@ -211,13 +211,15 @@ int bbm_hip_rng_init(bbm_hip_rng* rng, uint64_t seed, uint64_t lower, uint64_t u
   mt_seed(rng, seed);
   rng->lower = lower;
   rng->upper = upper;
+  rng->magic = BBM_HIP_RNG_MAGIC;
   return BBM_HIP_OK;
 }
 
 int bbm_hip_rng_draw(bbm_hip_rng* rng, uint64_t* out, size_t n)
 {
   if (!rng || (n > 0 && !out)) return fail(BBM_HIP_ERR_INVALID_ARG, "rng / out is NULL");
-  if (rng->pos > uint64_t(kN) || rng->upper < rng->lower) return fail(BBM_HIP_ERR_INVALID_ARG, "rng not initialised");
+  if (rng->magic != BBM_HIP_RNG_MAGIC || rng->pos > uint64_t(kN) || rng->upper < rng->lower)
+    return fail(BBM_HIP_ERR_INVALID_ARG, "rng not initialised (bbm_hip_rng_init)");
   for (size_t i = 0; i < n; ++i) out[i] = uniform(rng);
   return BBM_HIP_OK;
 }

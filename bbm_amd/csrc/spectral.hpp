@@ -206,6 +206,16 @@ struct Bagher
       else
       {
         // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154): exp(-t) / t^p with t = alpha + tan^2 / alpha
+        if (!(alpha[j] >= 0x1p-126f && alpha[j] < __builtin_inff() && __builtin_isfinite(p[j]))) [[unlikely]]
+        {
+          // a parameter outside the attribute's range (the reference accepts any alpha / p): the general forms --
+          // IEEE quotients, glibc's powf with its negative-base and special-operand rules, expf with overflow.  The
+          // parameters are uniform per launch (per probe in the loss), so this branch never splits a wave.
+          const float t = alpha[j] + g.tan2 / alpha[j];
+          const float den = powf_glibc_any(t, p[j]);
+          P22[j] = (den > kEpsF) ? expf_glibc(-t) / den : 0.0f;
+          continue;                                              // (never cached: only valid parameters fill it)
+        }
         const float t = alpha[j] + div_nr(g.tan2, alpha[j]);
         if constexpr (EXACT || EXACT_D)
         {

@@ -181,11 +181,11 @@ class SampledLoss:
         return self.total
 
     def materialized(self):
-        """This rank's shard as (pairs, reference table, n): the pairs computed once if the loss streams them from the
-        linearizer (materialize=False)."""
-        if self.pairs is None:
-            self.pairs = self.lin.directions(self.begin, self.n, self.stream)
-        return self.pairs, self.ref, self.n
+        """This rank's shard as (pairs, reference table, n).  A loss that streams its pairs from the linearizer
+        (materialize=False) computes them into a temporary the caller holds (24 B per sample while it lives): the loss
+        itself stays on the streaming kernel and keeps no copy."""
+        pairs = self.pairs if self.pairs is not None else self.lin.directions(self.begin, self.n, self.stream)
+        return pairs, self.ref, self.n
 
     def _workspace(self, nprobes, n=None):
         torch = _torch()
@@ -340,7 +340,10 @@ class Batch:
     def _gather(self, index):
         """This rank's samples among the global indices `index`, gathered densely -> (pairs, ref, n)."""
         torch = _torch()
-        pairs, ref, n = self.loss.materialized()
+        if getattr(self, "_shard", None) is None:
+            # the shard's pairs for this batch's gathers (a temporary for a streaming loss, held by the batch only)
+            self._shard = self.loss.materialized()
+        pairs, ref, n = self._shard
         begin = self.loss.begin
         idx = np.asarray(index, np.uint64)
         mine = idx[(idx >= begin) & (idx < begin + n)] - np.uint64(begin)
@@ -398,8 +401,20 @@ class Batch:
         return float(dt(s))
 
 
+def _update(loss):
+    """loss.update() where the loss has one (concepts::sampledlossfunction's update(), sampledlossfunction.h:52,
+    batch.h:48-54); a loss object without it -- only probe_losses(probes) and __call__(params) -- needs none."""
+    fn = getattr(loss, "update", None)
+    if fn is not None:
+        fn()
+
+
 class Compass:
     """compass<LOSSFUNC, PARAM> (include/optimizer/compass.h:40-183), probes batched on the GPU.
+
+    The loss protocol: probe_losses(probes) -> one loss per row of probes (a compass step's 2P probes in one call),
+    __call__(params) -> the loss at one full parameter vector, and optionally update() (called before each step and
+    by reset(), as compass.h:102-103 / :145-150 call the loss's).
 
     Optimises model.parameter_values(flag) (default bsdf_attr::All: Dependent attributes are held
     fixed) inside [lower, upper] (default: the model's parameter bounds); the model's parameters
@@ -438,8 +453,8 @@ class Compass:
         """compass.h:145-150: step size back to the initial one, the loss's update(), loss of the current
         parameters."""
         self.step_size = self.initial_step
-        self.loss.update()
-        self.loss_value = self.V(self.loss(params=self.full))
+        _update(self.loss)
+        self.loss_value = self.V(self.loss(self.full))
 
     def is_converged(self):
         return bool(self.step_size < self.tolerance)
@@ -452,7 +467,7 @@ class Compass:
         V = self.V
         if self.is_converged():
             return V(0)
-        self.loss.update()                      # compass.h:102-103, before the probes
+        _update(self.loss)                      # compass.h:102-103, before the probes
         param = self._params()
         s = self.step_size
         probes, in_box = [], []

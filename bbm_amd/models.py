@@ -9,8 +9,9 @@ constructor per model name taking the attributes as keyword arguments
 
 Here the attribute *layout* (names and shapes, in declaration order) lives in this table; the
 default values and bounds come from libbbm_hip itself (bbm_hip_model_params) so the library is
-the single source of truth for what the kernels expect.  Both are pinned against the reference's
-own values in tests/golden/models.json (tests/test_models.py).
+the single source of truth for what the kernels expect.  Both are pinned against the reference itself
+(oracle/_ref: tests/test_abi.py::test_registry_matches_reference, ::test_python_mirror_layout_covers_every_reference_model,
+::test_param_attrs_match_reference).
 """
 
 # attribute layout per model: list of (name, shape); shape () = scalar, (3,) = RGB/Spectrum,

@@ -2,7 +2,7 @@
 """bench.py -- BASELINE.json metric: CookTorrance eval+pdf pairs/s, 100M pairs per GPU, f32.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong] [--pairs P] [--model NAME]
-                    [--no-cpu] [--workload evalpdf|models|sample|fit|f64|selftest]
+                    [--no-cpu] [--workload evalpdf|models|sample|fit|f64|lambertian-cpu|selftest]
 
 One step = one fused eval+pdf pass (bbm_hip_eval_pdf) of the model over the GPU's shard of synthetic
 direction pairs already resident in HBM (SoA f32, generated on the device by the counter-based
@@ -76,11 +76,13 @@ def parse(argv=None):
     ap.add_argument("--graph-below", type=int, default=30_000_000)
     ap.add_argument("--fit-max-steps", type=int, default=200000, help="fit: compass steps cap for the convergence run")
     ap.add_argument("--fit-max-seconds", type=float, default=120.0, help="fit: wall-time cap for the convergence run")
-    ap.add_argument("--workload", default="evalpdf", choices=["evalpdf", "models", "sample", "fit", "f64", "selftest"],
+    ap.add_argument("--workload", default="evalpdf",
+                    choices=["evalpdf", "models", "sample", "fit", "f64", "lambertian-cpu", "selftest"],
                     help="evalpdf: the BASELINE metric (config 2, default); models: every model's eval over shared "
                          "pairs (config 3); sample: importance-sample -> eval -> pdf MC loop (config 4); fit: "
                          "multi-probe fitting loss of a compass step over the MERL grid (config 5); f64: the doubleRGB "
-                         "path (--model over --pairs f64 pairs + every doubleRGB model); selftest: the "
+                         "path (--model over --pairs f64 pairs + every doubleRGB model); lambertian-cpu: config 1, the "
+                         "native CPU backbone's Lambertian eval over 1M pairs (no GPU); selftest: the "
                          "multi-rank harness on the CPU (gloo), no GPU")
     return ap.parse_args(argv)
 
@@ -119,6 +121,48 @@ def cpu_baseline(model, din, dout, seconds):
                       f"on {cpu_model}"}
 
 
+def lambertian_cpu(args):
+    """Config 1 (BASELINE.json configs[0]): Lambertian eval on the native CPU backbone, 1M (in, out) pairs -- plumbing,
+    no GPU.  The reference itself (oracle/_ref: the reference headers with the native floatRGB backbone; oracle/port, the
+    C restatement, where the prebuilt shim is absent) evaluates the same counter-generated pairs the GPU path would
+    (tests/oracle_util.dirgen_numpy restates bbm_hip_fill_directions), K timed passes after W untimed ones, OpenMP over
+    every CPU this process may use; the single-thread rate beside it."""
+    from tests import oracle_util as ou
+    from tools.bench_configs import cpu_threads, _ref_eval_call
+    n = 1_000_000
+    din = np.ascontiguousarray(ou.dirgen_numpy(SEED, 0, 0, n, mode=0))
+    dout = np.ascontiguousarray(ou.dirgen_numpy(SEED, 1, 0, n, mode=0))
+    params = np.array([0.5, 0.5, 0.5], np.float32)      # Lambertian's default albedo (lambertian.h:27)
+    lib, kind = ou.ref(), "reference"
+    if lib is None:
+        lib, kind = ou.port(), "port"
+        fn = lib.bbmport_eval_pdf
+        import types
+        lib = types.SimpleNamespace(bbmref_eval_pdf=fn)
+    threads, tdesc = cpu_threads()
+    res = {}
+    for t in (threads, 1):
+        call = _ref_eval_call(lib, "Lambertian", params, din, dout, 1, t)
+        steps = args.steps if t == threads else max(3, args.steps // 20)
+        for _ in range(args.warmup if t == threads else 1):
+            call()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        res[t] = (steps, time.perf_counter() - t0)
+    steps, el = res[threads]
+    print(json.dumps({"metric": "Lambertian evals/s, native CPU backbone, 1M (in, out) pairs (config 1)",
+                      "value": n * steps / el, "unit": "pairs/s", "n_gpus": 0, "steps": steps, "warmup": args.warmup,
+                      "ms_per_step": el * 1e3 / steps, "higher_is_better": True, "scaling": "none",
+                      "vs_baseline": None, "dtype": "f32",
+                      "data": "synthetic (the counter-based directions of bbm_hip_fill_directions, restated in numpy)",
+                      "config": {"workload": f"Lambertian eval (no pdf) over {n} pairs on the host CPU, {kind} "
+                                             f"(oracle/_ref = the reference headers, native floatRGB backbone)",
+                                 "pairs": n, "parallelism": f"OpenMP {threads} threads"},
+                      "cores": threads, "cpu": tdesc, "kind": kind,
+                      "single_thread": {"value": n * res[1][0] / res[1][1], "steps": res[1][0]}}), flush=True)
+
+
 def selftest(args, dist, rank, world):
     """Harness only: a trivial CPU step under the same launch / barrier / max-over-ranks timing, with the evalpdf
     workload's --graph choice (a 'graph' here is R steps issued by one call, R = bh.graph_reps(K))."""
@@ -154,6 +198,9 @@ def main(argv=None):
         # no GPU call has been made in this process: start the ranks as a child and exit with its status
         sys.exit(bh.launch(args.gpus, os.path.abspath(__file__), sys.argv[1:] if argv is None else argv))
     world, rank, local = bh.world_from_env(args.gpus)
+    if args.workload == "lambertian-cpu":
+        lambertian_cpu(args)
+        return
     if args.workload == "selftest":
         dist = bh.init(world, local, "gloo")
         selftest(args, dist, rank, world)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define BBM_HIP_ABI_VERSION 11
+#define BBM_HIP_ABI_VERSION 12
 
 /* return codes */
 #define BBM_HIP_OK 0
@@ -71,8 +71,15 @@ const char* bbm_hip_last_error(void);
  * GGX's takes glibc's sinf / cosf of its azimuth (ndf/ggx.h:99) instead of the device library's (+28 % / +7 % on
  * importance-sampled reflectance).  Off: those quotients use the f32 remainder step, Bagher's D the fast power and
  * the samplers the device functions; outputs may differ in the last bits (the per-lane parity bar holds either way).
- * Returns the previous setting (0 / 1), or a negative code. */
+ * Returns the previous setting (0 / 1), or a negative code.  The switch is the process-wide DEFAULT: a call whose
+ * model id carries BBM_HIP_CALL_EXACT (or BBM_HIP_CALL_DEFAULT) runs in exact (or default) mode whatever the switch
+ * says, so a caller that must not depend on another thread's setting passes one of the two bits (re-entrant: the
+ * bit is decoded per call, on the calling thread).  The bits may be OR-ed into the id given to any entry point that
+ * takes a model id (eval / pdf / eval_pdf / sample / reflectance, loss, check; a child's id in a tree applies to
+ * that child); they are ignored by the doubleRGB kernels, which have no exact mode. */
 int bbm_hip_set_exact_subnormals(int on);
+#define BBM_HIP_CALL_EXACT 0x20000000
+#define BBM_HIP_CALL_DEFAULT 0x10000000
 
 /* Model registry.  Replaces the compile-time registry of BBM_EXPORT_BSDFMODEL
  * (e.g. include/bsdfmodel/cooktorrance.h:42) and the keyword lookup of
@@ -371,7 +378,9 @@ typedef struct bbm_hip_rng
   uint64_t mt[312];
   uint64_t pos;
   uint64_t lower, upper;
+  uint64_t magic;                          /* BBM_HIP_RNG_MAGIC once bbm_hip_rng_init has run; draw rejects others */
 } bbm_hip_rng;
+#define BBM_HIP_RNG_MAGIC 0x62626d726e673132ull
 int bbm_hip_rng_init(bbm_hip_rng* rng, uint64_t seed, uint64_t lower, uint64_t upper);
 int bbm_hip_rng_draw(bbm_hip_rng* rng, uint64_t* out, size_t n);     /* out: host memory */
 /* The default seed of bbm::rng (std::mt19937_64::default_seed) */

@@ -13,6 +13,8 @@
 
 #include <math.h>
 #include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #define PI_D 3.141592653589793238462643383279502884
 #define INV_PI_D 0.318309886183790671537767526745028724
@@ -436,6 +438,65 @@ int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n)
       case 8: out[i] = atan2f(a[i], b[i]); break;
       default: return -1;
     }
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * EPD's shadowing table: the arithmetic of the reference's generator precompute/HolzschuchPacanowski/G1.cpp
+ * (P2 :91-113, G1series :174-223, rows :280-300) in floatRGB, one row p = 5 / (row + 1) at a time.  contract != 0
+ * evaluates the three products GCC contracts into FMAs when the generator is built with FMA available and the
+ * default -ffp-contract=fast of gnu++20 (x86-64-v3; objdump of that build shows exactly these three vfmadd): P2's
+ * `r2 + q*q` (:107) and `integral += delta_q * exp(...)` (:107), and the series' `integral[j] += (r*t - 1) * p2`
+ * (:205).  With contract = 1 every entry of a row equals the shipped include/precomputed/holzschuchpacanowski/G1.h;
+ * with contract = 0 (each op rounded on its own) 3.6 % of the table differs in the 6th printed digit
+ * (tests/test_oracle.py::test_epd_g1_generator_recipe).  out: 1000 floats, each the "%g" (ostream << float,
+ * precision 6) print of G1 read back as the header's literal is. */
+static float g1_conv_f(float x) { return powf(logf(1.0f / x), 20.0f); }
+static double g1_conv_d(double x) { return pow(log(1.0 / x), (double)20.0f); }
+
+int bbmport_epd_g1_row(int row, int contract, float* out)
+{
+  if (row < 0 || row >= 100 || !out) return -1;
+  const float p = (float)(5.0 / (double)(float)(row + 1));
+  const float norm = (float)((double)p / ((double)kPiF * tgamma(1.0 / (double)p)));
+  float integral[1000];
+  integral[0] = 0.0f;
+  float prev = 0.0f, Pj = 0.0f;
+  const float delta_x = 1.0f / 1000.0f;
+  for (int j = 1; j < 1000; ++j)
+  {
+    const float x = (float)(j + 1) / 1000.0f;
+    const float t = 1.0f / g1_conv_f(x);
+    if (isinf(t)) { integral[j] = t; continue; }
+    const float dr = g1_conv_f(x - delta_x) - g1_conv_f(x);
+    const float r = (float)g1_conv_d((double)x - 0.5 * (double)delta_x);
+    /* P2(r, p) */
+    const float r2 = r * r;
+    const float deltax = 0.0001f;
+    float s = 0.0f;
+    for (float xx = 1.0f; xx > deltax; xx -= deltax)
+    {
+      const float dq = g1_conv_f(xx - deltax) - g1_conv_f(xx);
+      const float q = (float)g1_conv_d((double)xx - 0.5 * (double)deltax);
+      if (isnan(dq)) continue;
+      const float base = contract ? fmaf(q, q, r2) : r2 + q * q;
+      const float e = expf(-powf(base, p));
+      s = contract ? fmaf(dq, e, s) : s + dq * e;
+    }
+    const float p2 = (float)(2.0 * (double)norm * (double)s) * dr;
+    float v = 0.0f;
+    if (prev > 0) v = (integral[j - 1] + Pj) * t / prev - Pj;
+    if (r * t > 1) v = contract ? fmaf(r * t - 1, p2, v) : v + (r * t - 1) * p2;
+    integral[j] = v;
+    prev = t;
+    Pj += p2;
+  }
+  for (int j = 0; j < 1000; ++j)
+  {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%g", (double)(float)(1.0 / (1.0 + (double)integral[j])));
+    out[j] = (float)strtod(buf, NULL);
   }
   return 0;
 }

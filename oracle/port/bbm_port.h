@@ -37,6 +37,11 @@ int bbmport_sample(const char* name, const float* params, int nparams, size_t n,
  * native backbone calls, for pinning the device restatements (bbm_hip_libm_eval) on the same machine */
 int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n);
 
+/* one row (p = 5 / (row + 1)) of EPD's shadowing table as the reference's generator computes it
+ * (precompute/HolzschuchPacanowski/G1.cpp), printed to 6 digits and read back; contract != 0: with the FMA
+ * contractions of the build that produced the shipped G1.h (see bbm_port.c).  out: 1000 floats. */
+int bbmport_epd_g1_row(int row, int contract, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,7 +44,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.bbm_hip_abi_version() == 11
+    assert lib.bbm_hip_abi_version() == 12
 
 
 def test_f64_registry(lib):

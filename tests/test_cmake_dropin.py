@@ -36,6 +36,6 @@ def test_backbone_plugs_into_reference_cmake(tmp_path):
     r = subprocess.run([str(build / "consumer")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d == {"abi": 11, "cooktorrance": "CookTorrance", "nested_children": 2, "failures": 0}
+    assert d == {"abi": 12, "cooktorrance": "CookTorrance", "nested_children": 2, "failures": 0}
     # the configure step wrote its generated header into the copy, not into the reference
     assert (src / "include" / "bbm_bsdfmodels.h").exists()

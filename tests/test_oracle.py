@@ -207,3 +207,31 @@ def test_theta_restatement_matches_glibc():
     13th float chord length in [0, 2], both hemispheres (stride 1: all 1.07e9, 0 mismatches)."""
     out = _run_check("theta_check", 13)
     assert " 0 mismatches" in out, out
+
+
+@pytest.mark.skipif(ou.ref() is None, reason="oracle/_ref not built")
+def test_epd_g1_generator_recipe():
+    """The shipped EPD shadowing table (include/precomputed/holzschuchpacanowski/G1.h, read through the compiled
+    reference) is what precompute/HolzschuchPacanowski/G1.cpp prints when GCC contracts its three multiply-adds
+    into FMAs (built with FMA available and gnu++20's default -ffp-contract=fast: the whole generated header then
+    equals G1.h byte for byte in every entry, found by compiling G1.cpp here under candidate recipes).  The C
+    restatement (oracle/port, bbmport_epd_g1_row) with those contractions reproduces sampled rows exactly; without
+    them a fifth of a row differs in the 6th printed digit.  libbbm_hip's on-device generator follows the
+    contracted recipe (bbm_amd/csrc/inst_epd.hip; GPU: test_epd_g1_table_matches_reference)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    port, ref = ou.port(), ou.ref()
+    want = np.zeros(100000, np.float32)
+    assert ref.bbmref_epd_g1(want.ctypes.data_as(ctypes.c_void_p), want.size) == want.size
+
+    def row(args):
+        r, contract = args
+        out = np.zeros(1000, np.float32)
+        assert port.bbmport_epd_g1_row(r, contract, out.ctypes.data_as(ctypes.c_void_p)) == 0
+        return np.mean(out == want[r * 1000:(r + 1) * 1000])
+
+    cases = [(0, 1), (2, 1), (17, 1), (54, 1), (99, 1), (2, 0)]
+    with ThreadPoolExecutor(6) as ex:
+        same = list(ex.map(row, cases))
+    assert same[:5] == [1.0] * 5, same
+    assert same[5] < 0.9, same

@@ -16,6 +16,15 @@
   f64     the doubleRGB configuration (bbm_hip_eval_pdf_f64): --model's eval+pdf over --pairs f64 pairs per GPU, 80 B
           per pair algorithmic (48 B in + 32 B out), and every model with doubleRGB kernels over 10M shared pairs.
 Timing follows bench.py: warmup, barrier + synchronize around K timed steps, max over ranks.
+
+cpu_baseline (rank 0, N = 1, unless --no-cpu): the reference itself (oracle/_ref/libbbm_ref.so: the reference headers
+compiled with the native floatRGB backbone, OpenMP over every CPU this process may use, as bench.py's headline leg) on a
+bounded sample of the same workload, about --cpu-seconds of CPU work per line:
+  models  every model's eval (mode eval only) over a sample of the same pairs, ~--cpu-seconds / #models each
+  sample  the reference's own loop (bin/checkBsdf.cpp:78-84): bsdf.sample(out, xi) then bsdf.eval(dir, out) per sample
+  fit     sampledlossfunction::operator()(idx) (include/bbm/sampledlossfunction.h:62-73) over every pair of the MERL
+          grid, once per probe -- the reference evaluates the fitted and the reference model per sample each time
+lambertian-cpu (config 1, bench.py): the native backbone's Lambertian eval over 1M pairs, no GPU.
 """
 import ctypes
 import json
@@ -112,6 +121,151 @@ def _graph(launch, reps):
 MODEL_SETS = 4
 
 
+# ---------------------------------------------------------------- CPU baselines (the reference on the host)
+
+def cpu_threads():
+    """(threads, description): every CPU this process may use -- the affinity mask capped by the cgroup CPU quota
+    (bench.py cpu_baseline)."""
+    aff, phys, smt, quota, cpu_model = bh.cpu_topology()
+    threads = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
+    desc = (f"OpenMP {threads} threads = every CPU this process may use (affinity mask: {aff} threads on {phys} "
+            f"physical cores x {smt} SMT{'' if quota is None else f'; cgroup CPU quota {quota:g} CPUs'}) on {cpu_model}")
+    return threads, desc
+
+
+def _cpu_lib():
+    """(library, kind): the compiled reference (oracle/_ref) or, without it, the C restatement (oracle/port: the
+    models it covers only)."""
+    from tests import oracle_util as ou
+    if ou.ref() is not None:
+        return ou.ref(), "reference"
+    return None, "port"
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _timed_calls(call, budget_s):
+    """call() once untimed, then repeatedly until budget_s has passed -> (calls, seconds)."""
+    call()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        call()
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            return done, el
+
+
+def _ref_eval_call(lib, name, params, hin, hout, mode, threads, merl_path=None):
+    """A closure running the reference's eval (mode 1) / eval+pdf (3) over the host SoA pairs into preallocated rows."""
+    n = hin.shape[1]
+    out = np.zeros((4, n), np.float32)
+    p = np.ascontiguousarray(params, np.float32)
+    args = (ctypes.c_size_t(n), _fp(hin[0]), _fp(hin[1]), _fp(hin[2]), _fp(hout[0]), _fp(hout[1]), _fp(hout[2]),
+            ctypes.c_uint32(3), ctypes.c_uint32(0), mode, _fp(out[0]), _fp(out[1]), _fp(out[2]), _fp(out[3]), threads)
+    if merl_path is not None:
+        fn = lambda: lib.bbmref_merl_eval_pdf(merl_path.encode(), *args)          # noqa: E731
+    else:
+        fn = lambda: lib.bbmref_eval_pdf(name.encode(), _fp(p), p.size, *args)    # noqa: E731
+
+    def call():
+        if fn() != 0:
+            raise KeyError(f"reference has no model {name}")
+    return call
+
+
+def cpu_models(names, din, dout, seconds, merl_path=None):
+    """Config 3's CPU column: the reference's eval of every model over a sample of the benchmark's pairs, about
+    seconds / len(names) each; per-model pairs/s and the whole set's rate (sum of pairs / sum of times)."""
+    lib, kind = _cpu_lib()
+    if lib is None:
+        return None
+    threads, tdesc = cpu_threads()
+    n_base = min(din.shape[1], 1 << 18)
+    per, tot_pairs, tot_s = {}, 0, 0.0
+    budget = max(seconds / max(len(names), 1), 0.2)
+    for name in names:
+        if name == "Merl" and merl_path is None:
+            continue
+        n = min(din.shape[1], 1 << 21) if name == "Merl" else n_base   # amortise the shim's per-call file read
+        hin = np.ascontiguousarray(din[:, :n].cpu().numpy())
+        hout = np.ascontiguousarray(dout[:, :n].cpu().numpy())
+        params = bbm_amd.BsdfModel(name).parameter_values() if name != "Merl" else None
+        call = _ref_eval_call(lib, name, params, hin, hout, 1, threads, merl_path if name == "Merl" else None)
+        calls, el = _timed_calls(call, budget)
+        per[name] = {"pairs_per_s": calls * n / el, "sample_pairs": n, "calls": calls, "seconds": el}
+        tot_pairs += calls * n
+        tot_s += el
+    return {"value": tot_pairs / tot_s, "unit": "pairs/s", "cores": threads, "kind": kind,
+            "sample": f"eval (no pdf) of each of {len(per)} models over the first {n_base} pairs of the benchmark's "
+                      f"operand set 0 (Merl: {min(din.shape[1], 1 << 21)} pairs, the shim reading the .binary per call), "
+                      f"repeated for ~{budget:.2f} s per model; value = all pairs / all seconds; via oracle/_ref "
+                      f"(reference headers, native floatRGB); {tdesc}",
+            "per_model": per}
+
+
+def cpu_sample(names, outs, slots, seconds):
+    """Config 4's CPU column: the reference's importance-sampled reflectance loop (bin/checkBsdf.cpp:78-84: sample
+    then eval at the sampled direction, accumulated where pdf > Epsilon) over a bounded sample per model."""
+    lib, kind = _cpu_lib()
+    if lib is None:
+        return None
+    threads, tdesc = cpu_threads()
+    n = 1 << 20
+    rng = np.random.default_rng(SEED)
+    o = np.ascontiguousarray(np.repeat(outs.cpu().numpy(), n // slots, axis=1))
+    xi = rng.random((2, n), dtype=np.float32)
+    per = {}
+    for name in names:
+        p = np.ascontiguousarray(bbm_amd.BsdfModel(name).parameter_values(), np.float32)
+        d = np.zeros((4, n), np.float32)
+        flag = np.zeros(n, np.uint32)
+        ev = np.zeros((4, n), np.float32)
+
+        def call():
+            rc = lib.bbmref_sample(name.encode(), _fp(p), p.size, ctypes.c_size_t(n), _fp(o[0]), _fp(o[1]), _fp(o[2]),
+                                   _fp(xi[0]), _fp(xi[1]), ctypes.c_uint32(3), ctypes.c_uint32(0), _fp(d[0]), _fp(d[1]),
+                                   _fp(d[2]), _fp(d[3]), _fp(flag), threads)
+            assert rc == 0
+            rc = lib.bbmref_eval_pdf(name.encode(), _fp(p), p.size, ctypes.c_size_t(n), _fp(d[0]), _fp(d[1]), _fp(d[2]),
+                                     _fp(o[0]), _fp(o[1]), _fp(o[2]), ctypes.c_uint32(3), ctypes.c_uint32(0), 1,
+                                     _fp(ev[0]), _fp(ev[1]), _fp(ev[2]), _fp(ev[3]), threads)
+            assert rc == 0
+            keep = d[3] > np.float32(np.finfo(np.float32).eps)
+            (ev[:3, keep] * (d[2, keep] / d[3, keep])).sum(axis=1)
+        calls, el = _timed_calls(call, seconds / max(len(names), 1))
+        per[name] = {"samples_per_s": calls * n / el, "calls": calls, "seconds": el}
+    head = next(iter(per))
+    return {"value": per[head]["samples_per_s"], "unit": "samples/s", "cores": threads, "kind": kind,
+            "sample": f"{n} samples per call ({slots} theta_out x {n // slots}, xi from numpy), the reference's "
+                      f"sample -> eval -> z / pdf accumulation as checkBsdf's reflectance test, repeated for "
+                      f"~{seconds / max(len(names), 1):.1f} s per model; value = {head}; via oracle/_ref; {tdesc}",
+            "per_model": per}
+
+
+def cpu_fit(name, fitted, reference, lin, seconds):
+    """Config 5's CPU column: the reference's sampledlossfunction over the same MERL-grid pairs, one probe per call
+    (operator()(idx) for every idx, OpenMP; each sample evaluates the fitted and the reference model, as the
+    reference does), for about `seconds`."""
+    lib, kind = _cpu_lib()
+    if lib is None:
+        return None
+    from tests import oracle_util as ou
+    threads, tdesc = cpu_threads()
+    din, dout = lin.directions()
+    hin, hout = din.cpu().numpy(), dout.cpu().numpy()
+    fp = fitted.parameter_values()
+    rp = reference.parameter_values()
+    calls, el = _timed_calls(lambda: ou.ref_pair_losses(name, fp, rp, hin, hout, 3, nthreads=threads), seconds)
+    n = hin.shape[1]
+    return {"value": calls * n / el, "unit": "probe-pairs/s", "cores": threads, "kind": kind,
+            "sample": f"{calls} probes x the {n} MERL-grid pairs (standardLog), reference = the analytic fit "
+                      f"(fits/{FIT_MATERIAL[0]}:3), ~{seconds:.0f} s; the reference's sampledlossfunction evaluates "
+                      f"both models per sample and probe; via oracle/_ref; {tdesc}"}
+
+
 def bench_models(args, dist, rank, world):
     """Config 3.  Every model's eval over 10M pairs per GPU, timed as HIP-graph replays of GRAPH_REPS launches that
     cycle over MODEL_SETS distinct input/output sets (360 MB each, 1.44 GB in all): no launch finds its operands in
@@ -158,6 +312,15 @@ def bench_models(args, dist, rank, world):
             # VALU-bound models: the fraction of the chip's VALU issue slots, from committed counters of this kernel
             per[name]["valu_roofline"] = vr
         total_t += elapsed / reps
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        with tempfile.TemporaryDirectory() as tmp:
+            merl_path = None
+            if "Merl" in names:
+                merl_path = os.path.join(tmp, "synthetic.binary")
+                ld, lo = fit.merl_linearizer().directions()
+                merl.write_binary(merl_path, merl.encode(bbm_amd.CookTorrance().eval(ld, lo).cpu().numpy()))
+            cpu = cpu_models(names, sets[0][0], sets[0][1], args.cpu_seconds, merl_path)
     if rank == 0:
         _line(args, world, "BSDF evals/s (eval), all single bsdfmodels, 10M shared pairs per GPU (config 3)",
               len(names) * n * world * args.steps / total_t, "pairs/s", total_t / len(names),
@@ -165,7 +328,7 @@ def bench_models(args, dist, rank, world):
                            f"graph of {reps} launches per step over {MODEL_SETS} distinct input/output sets, "
                            f"{MODEL_SETS * 36 * n / 1e9:.2f} GB > the 256 MiB Infinity Cache)",
                "pairs_per_gpu": n, "operand_sets": MODEL_SETS, "parallelism": f"dp{world} (independent shards)"},
-              {"scaling": "weak", "per_model": per})
+              dict({"scaling": "weak", "per_model": per}, **({"cpu_baseline": cpu} if cpu else {})))
 
 
 # models of config 4 whose sampler has an exact-mode twin (math.hpp exact_sample_t: Beckmann's glibc erff / logf,
@@ -216,6 +379,9 @@ def bench_sample(args, dist, rank, world):
                      "estimate_vs_reflectance": [[float(x) for x in est[k]] + [float(y) for y in refl[k]] for k in (0, slots - 1)]}
         total_t += elapsed
         elapsed_of[name] = elapsed
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_sample(list(res), outs, slots, args.cpu_seconds)
     if rank == 0:
         # the workload value is the first model's own rate (CookTorrance, the headline model), not an average over
         # the models timed; every model's figure is in per_model
@@ -225,8 +391,8 @@ def bench_sample(args, dist, rank, world):
               {"workload": f"checkBsdf reflectance test, importance sampling, {slots} theta_out x "
                            f"{per_gpu // slots} samples per GPU, in-kernel reduction",
                "samples_per_gpu": per_gpu, "parallelism": f"dp{world} (sample shards, one gather at the end)"},
-              {"scaling": "weak", "per_model": res,
-               "roofline": res[head]["roofline"]})
+              dict({"scaling": "weak", "per_model": res, "roofline": res[head]["roofline"]},
+                   **({"cpu_baseline": cpu} if cpu else {})))
 
 
 def _merl_from(source):
@@ -288,6 +454,9 @@ def bench_fit(args, dist, rank, world):
         steps += 1
     torch.cuda.synchronize()
     fit_s = time.perf_counter() - t0
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_fit(name, fitted, material, lin, args.cpu_seconds)
     if rank == 0:
         pairs = lin.size()
         _line(args, world, "fitting-loss probe-pair evals/s, Aggregate(Lambertian, Bagher), MERL grid, 2P probes per "
@@ -305,7 +474,8 @@ def bench_fit(args, dist, rank, world):
                        "converged": comp.is_converged(), "max_steps": args.fit_max_steps,
                        "max_seconds": args.fit_max_seconds, "seconds": fit_s,
                        "ms_per_compass_step": fit_s * 1e3 / max(steps, 1), "loss_start": loss0,
-                       "loss_end": float(comp.loss_value), "final_step_size": float(comp.step_size)}})
+                       "loss_end": float(comp.loss_value), "final_step_size": float(comp.step_size)},
+               **({"cpu_baseline": cpu} if cpu else {})})
 
 
 def bench_f64(args, dist, rank, world):

@@ -19,7 +19,7 @@ mkdir -p gpurun_out
 SQ8="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64"
 LANE="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES"
 # PMC_WAIT=1: a third pass -- where the wave cycles go (parked on s_waitcnt, issue-stalled, issuing) and the
-# GPU-busy cycles (GRBM_GUI_ACTIVE / dispatch time = the clock the kernel ran at)
+# GPU-busy cycles (GRBM_GUI_ACTIVE summed over the 8 XCDs: / 8 / dispatch time = the clock the kernel ran at)
 WAIT="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
 
 step_tests() {
@@ -94,7 +94,7 @@ print(sys.argv[3], "valu/unit %.0f" % (v * 64 / u), "issue %.3f" % (v / (c["disp
 if "SQ_WAIT_ANY" in c:
     w = max(c.get("SQ_WAVE_CYCLES", 1), 1)
     print("   wait %.3f inst-stall %.3f active %.3f  clock %.2f GHz" % (c["SQ_WAIT_ANY"] / w, c["SQ_WAIT_INST_ANY"] / w,
-          c["SQ_ACTIVE_INST_ANY"] / w, c.get("GRBM_GUI_ACTIVE", 0) / c["dispatch_ns"]))
+          c["SQ_ACTIVE_INST_ANY"] / w, c.get("GRBM_GUI_ACTIVE", 0) / 8 / c["dispatch_ns"]))
 EOF
     rm -rf "${out:?}/$M"/*/   # raw CSVs: the summary above is what is kept
   done
