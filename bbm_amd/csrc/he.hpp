@@ -28,21 +28,7 @@ constexpr float kPiSqFourF = (4.0f * kPiF) * kPiF;               // Constants::P
 // floatRGB::wavelength() (backbone/native/include/backbone.h:36), in micron
 constexpr float kWavelength[3] = {float(0.645), float(0.526), float(0.444)};
 
-// the CDF pointer rides in two parameter slots (bit pattern of a 64-bit address)
-__host__ __device__ __forceinline__ const float* param_ptr(const float* p, int slot)
-{
-  uint32_t lo, hi;
-  __builtin_memcpy(&lo, p + slot, 4);
-  __builtin_memcpy(&hi, p + slot + 1, 4);
-  return reinterpret_cast<const float*>((uint64_t(hi) << 32) | lo);
-}
-inline void set_param_ptr(float* p, int slot, const void* ptr)
-{
-  const uint64_t v = reinterpret_cast<uint64_t>(ptr);
-  const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
-  __builtin_memcpy(p + slot, &lo, 4);
-  __builtin_memcpy(p + slot + 1, &hi, 4);
-}
+// the CDF pointer rides in two parameter slots (param_ptr / set_param_ptr, kernels.hpp)
 
 // std::lerp for floats (libstdc++ <cmath>)
 __device__ __forceinline__ float std_lerpf(float a, float b, float t)
@@ -460,6 +446,11 @@ struct He
     const float nrm = div_nr(1.0f, (kPiF * in.z) * out.z);
 #pragma unroll
     for (int c = 0; c < 3; ++c) e.pre[c] = ((nrm * F[c]) * S) * Gv;
+#if defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG == 2
+    e.pre[0] = sigma(in, out); e.pre[1] = S; e.pre[2] = Gv;
+#elif defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG == 3
+    e.pre[0] = F[0]; e.pre[1] = F[1]; e.pre[2] = nrm;
+#endif
   }
 
   template<bool SCALE = true>
@@ -475,6 +466,11 @@ struct He
       rgb[c] = e.active ? v : 0.0f;
 #ifdef BBM_HIP_HE_COUNT_TERMS
       rgb[c] = Dv[c];
+#endif
+#if defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG == 1
+      rgb[c] = Dv[c];            // diagnostics build only (tools/dbg_he_parts.py): D per channel
+#elif defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG >= 2
+      rgb[c] = e.pre[c];         // diagnostics build only: (sigma, S, G) / (F red, F green, 1 / (pi z z)), eval_prep
 #endif
     }
   }

@@ -43,6 +43,23 @@ void scratch_release(void* p, hipStream_t s);
 
 struct ParamBlock { float v[kMaxParams]; };
 
+// a device address riding in two parameter slots (bit pattern of a 64-bit pointer): per-launch derived data such as
+// the He family's sampler CDF or EPD's shadowing-table row pair (host_params below)
+__host__ __device__ __forceinline__ const float* param_ptr(const float* p, int slot)
+{
+  uint32_t lo, hi;
+  __builtin_memcpy(&lo, p + slot, 4);
+  __builtin_memcpy(&hi, p + slot + 1, 4);
+  return reinterpret_cast<const float*>((uint64_t(hi) << 32) | lo);
+}
+inline void set_param_ptr(float* p, int slot, const void* ptr)
+{
+  const uint64_t v = reinterpret_cast<uint64_t>(ptr);
+  const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+  __builtin_memcpy(p + slot, &lo, 4);
+  __builtin_memcpy(p + slot + 1, &hi, 4);
+}
+
 // Per-model host work before a launch (e.g. building a lookup table on first use); no-op by default.
 template<class Model> struct host_prepare { static int run(hipStream_t) { return 0; } };
 

@@ -138,8 +138,8 @@ __device__ __forceinline__ float div_nr(float n, float d)
 
 // n / d correctly rounded on the subnormal grid as well (EXACT), for a finite normal d and any float n: the f32
 // reciprocal seed q = n rcp(d) (~2^-22 relative), one remainder step in double (n - d q is exact in double: a 48-bit
-// product and a cancelling difference), rounded once to float -- the IEEE float quotient except within ~2^-22 ulp of
-// a rounding midpoint, subnormal numerators and quotients included, where div_nr's f32 remainder is itself rounded
+// product and a cancelling difference), rounded once to float -- the IEEE float quotient (a subnormal or zero quotient
+// from the IEEE double quotient, below), subnormal numerators included, where div_nr's f32 remainder is itself rounded
 // to the subnormal grid.  For the sites where a subnormal intermediate can flow into a normal output (the Beckmann D
 // of a far-tail halfway vector and the two quotients downstream of it); EXACT = false is div_nr.  Selected per
 // launch (bbm_hip_set_exact_subnormals): measured +3.6-4.3 % on the headline kernel (0.703 -> 0.734, 0.726 -> 0.752 ms per 100 M pairs),
@@ -152,7 +152,16 @@ __device__ __forceinline__ float div_sub(float n, float d)
   {
     const float r = __builtin_amdgcn_rcpf(d);
     const double q0 = double(n * r);
-    return float(__builtin_fma(__builtin_fma(-double(d), q0, double(n)), double(r), q0));
+    float q = float(__builtin_fma(__builtin_fma(-double(d), q0, double(n)), double(r), q0));
+    // A quotient that is not a normal float can lie exactly on (or within the step's error of) a midpoint of the
+    // subnormal grid -- a normal one cannot: n = d m with m of 25 significant bits would need more than 24 bits in n
+    // -- so those lanes (a wave-uniform branch, rarely taken) take the IEEE double quotient instead, which rounds to
+    // the float grid exactly as the float division (53 >= 2 x 24 + 2, and a tie is exact in double).  Found by the
+    // exhaustive device sweep of erfcf (tests/test_gpu_libm.py: erfcf(10) = 1.5 x 2^-149 rounded to even).
+    const bool sub = __builtin_fabsf(q) < 0x1p-126f;
+    if (__builtin_amdgcn_ballot_w64(sub) != 0)
+      if (sub) q = float(double(n) / double(d));
+    return q;
   }
   else return div_nr(n, d);
 }

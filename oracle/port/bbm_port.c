@@ -500,3 +500,40 @@ int bbmport_epd_g1_row(int row, int contract, float* out)
   }
   return 0;
 }
+
+/* Exhaustive libm pins (tests/test_gpu_libm.py): the inputs are the float bit patterns start .. start + n - 1; got[i]
+ * is the device's value for pattern start + i (bbm_hip_libm_eval).  Returns the number of patterns whose host libm
+ * value differs bitwise (any NaN equals any NaN), and writes up to `cap` of them to bad[]. */
+long long bbmport_libm_sweep(int func, uint32_t start, size_t n, const float* got, uint32_t* bad, int cap, int nthreads)
+{
+  long long nbad = 0;
+  #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+  for (long long i = 0; i < (long long)n; ++i)
+  {
+    const uint32_t bits = start + (uint32_t)i;
+    float x;
+    memcpy(&x, &bits, 4);
+    float r;
+    switch (func)
+    {
+      case 0: r = expf(x); break;
+      case 1: r = logf(x); break;
+      case 3: r = erff(x); break;
+      case 4: r = erfcf(x); break;
+      case 6: r = sinf(x); break;
+      case 7: r = cosf(x); break;
+      default: r = x; break;
+    }
+    uint32_t a, b;
+    memcpy(&a, &r, 4);
+    memcpy(&b, &got[i], 4);
+    if (a != b && !(isnan(r) && isnan(got[i])))
+    {
+      long long k;
+      #pragma omp atomic capture
+      k = nbad++;
+      if (k < cap && bad) bad[k] = bits;
+    }
+  }
+  return nbad;
+}

@@ -42,6 +42,10 @@ int bbmport_libm(int func, const float* a, const float* b, float* out, size_t n)
  * contractions of the build that produced the shipped G1.h (see bbm_port.c).  out: 1000 floats. */
 int bbmport_epd_g1_row(int row, int contract, float* out);
 
+/* exhaustive sweep: host libm (func as bbmport_libm) on the float bit patterns start .. start + n - 1 against got[];
+ * returns the mismatch count, the first `cap` mismatching patterns in bad[] */
+long long bbmport_libm_sweep(int func, uint32_t start, size_t n, const float* got, uint32_t* bad, int cap, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,3 +6,4 @@
 #include "ref_check.cpp"
 #include "ref_merl.cpp"
 #include "ref_runtime.cpp"
+#include "ref_cli.cpp"

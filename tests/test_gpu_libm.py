@@ -153,3 +153,46 @@ def test_theta_bitexact(lib):
     want = np.where(z >= 0, te, np.float64(np.float32(np.pi)) - te).astype(f)
     bad = np.nonzero(~_same(got, want))[0]
     assert bad.size == 0, f"{bad.size} lanes differ, e.g. x={x[bad[:4]]} z={z[bad[:4]]} got={got[bad[:4]]} want={want[bad[:4]]}"
+
+
+CHUNK = 1 << 28
+# |x| < 120 for the sin / cos restatement (every float the reference's cossin reaches)
+SINCOS_HI = int(np.float32(120.0).view(np.uint32))
+EXHAUSTIVE = {"expf": [(0, 1 << 32)], "logf": [(0, 1 << 32)], "erff": [(0, 1 << 32)], "erfcf": [(0, 1 << 32)],
+              "sinf": [(0, SINCOS_HI), (1 << 31, (1 << 31) + SINCOS_HI)],
+              "cosf": [(0, SINCOS_HI), (1 << 31, (1 << 31) + SINCOS_HI)]}
+
+
+@pytest.mark.parametrize("func", list(EXHAUSTIVE))
+def test_device_libm_exhaustive(lib, func):
+    """Every float bit pattern (sinf / cosf: every |x| < 120) through the SHIPPED device code (bbm_hip_libm_eval ->
+    math.hpp) against this machine's libm, bit for bit (NaN = NaN): the device restatements are pinned exhaustively
+    themselves, not through a host transcription.  2^28 patterns per launch; the host side compares with OpenMP
+    (oracle/port: bbmport_libm_sweep)."""
+    from bbm_amd import _lib
+    port = ou.port()
+    port.bbmport_libm_sweep.restype = ctypes.c_longlong
+    total, nbad, bad = 0, 0, []
+    out = torch.empty(CHUNK, dtype=torch.float32, device="cuda")
+    buf = np.empty(CHUNK, np.float32)
+    badbuf = np.zeros(16, np.uint32)
+    for lo, hi in EXHAUSTIVE[func]:
+        for start in range(lo, hi, CHUNK):
+            n = min(CHUNK, hi - start)
+            bits = torch.arange(start, start + n, dtype=torch.int64, device="cuda")
+            bits = torch.where(bits >= (1 << 31), bits - (1 << 32), bits).to(torch.int32)
+            x = bits.view(torch.float32)
+            _lib.check(lib.bbm_hip_libm_eval(FUNCS[func], x.data_ptr(), None, out.data_ptr(), n, None))
+            torch.cuda.synchronize()
+            buf[:n] = out[:n].cpu().numpy()
+            k = port.bbmport_libm_sweep(FUNCS[func], ctypes.c_uint32(start), ctypes.c_size_t(n),
+                                        buf.ctypes.data_as(ctypes.c_void_p), badbuf.ctypes.data_as(ctypes.c_void_p),
+                                        16, 16)
+            if k and len(bad) < 16:
+                bad += [hex(int(b)) for b in badbuf[:min(k, 16)]]
+            nbad += k
+            total += n
+            del bits, x
+        print(f"{func}: [{lo:#x}, {hi:#x}) swept", flush=True)
+    print(f"{func}: {total} patterns, {nbad} differ from the host libm", flush=True)
+    assert nbad == 0, f"{func}: {nbad} of {total} patterns differ, e.g. {bad}"
