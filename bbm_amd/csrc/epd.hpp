@@ -162,41 +162,13 @@ __device__ __forceinline__ double gamma_q_inv_d(double a, double q)
   return x;
 }
 
-// The G1 lookup with a launch's two table rows interleaved (host_params<EpdM>, inst_epd.hip): p is uniform per
-// launch, so the bilinear lookup only ever reads rows f0 = floor(m0) and c0 = ceil(m0) (clamped); column c of `pair`
-// holds (G1[f0][c], G1[c0][c], G1[f0][c + 1], G1[c0][c + 1]) (c + 1 clamped to 999), so the four entries of a lookup
-// are one 16 B gather instead of four dependent 4 B gathers into the 400 KB table -- the same floats, the same
-// lerps, bit-identical.  Columns f1 and c1 = ceil(m1) are equal (m1 integral or clamped) or adjacent.
-__device__ __forceinline__ float epd_g1_pair_lookup(const float4* pair, double w0, float t)
-{
-  const float it = div_nr(1.0f, t);
-  const double L = (it == 0.0f) ? -__builtin_inf() : ((it > 3.40282347e38f) ? __builtin_inf()
-                   : ((it != it) ? double(it) : double(float(log2_acc(it) * 0.69314718055994530942))));
-  const double e1 = __builtin_isfinite(L) ? exp_dd(-exp_dd(L * 0.05)) : ((L > 0.0) ? 0.0 : 1.0);
-  const double m1 = (L != L) ? L : e1 * 1000.0 - 1.0;
-  const int f1 = int(fmin(fmax(floor(m1), 0.0), double(kEpdCols - 1)));
-  const int c1 = int(fmin(fmax(ceil(m1), 0.0), double(kEpdCols - 1)));
-  const float4 e = pair[f1];
-  const bool same = c1 == f1;
-  const double w1 = m1 - floor(m1);
-  const float lo = float(std_lerp(e.x, same ? e.x : e.z, w1));
-  const float hi = float(std_lerp(e.y, same ? e.y : e.w, w1));
-  return float(std_lerp(lo, hi, w0));
-}
-
 // ndf::epd (ndf/epd.h:43-186)
 struct EpdNdf
 {
   static constexpr int kParams = 2;
-  static constexpr int kPairSlot = 4;      // the row-pair buffer's address: after beta, p, n, k (EpdM's parameters)
   float beta, p, normalization, inv_p;
-  const float4* pair;                      // host_params<EpdM>'s per-launch row pair, or null (the whole table)
-  double w0;                               // m0 - floor(m0), m0 = 5 / p - 1 (the row weight, uniform)
   __device__ explicit EpdNdf(const float* q) : beta(q[0]), p(q[1])
   {
-    pair = reinterpret_cast<const float4*>(param_ptr(q, kPairSlot));
-    const double m0 = 5.0 / double(p) - 1.0;
-    w0 = m0 - floor(m0);
     // compute_normalization (epd.h:160-178): p InvPi rcp(tgamma(rcp(p))) / beta^2, 0 if p <= eps
     const float n = (p > kEpsF) ? (p * kInvPiF) * div_nr(1.0f, tgammaf(div_nr(1.0f, p))) : 0.0f;
     normalization = div_nr(n, beta * beta);
@@ -216,13 +188,7 @@ struct EpdNdf
   __device__ __forceinline__ float G1(v3 v, v3 m) const
   {
     const bool mask = (v.z > 0) && (dot3(v, m) > 0);
-#ifndef BBM_HIP_EPD_FULL_TABLE
-    float g;
-    if (pair) g = epd_g1_pair_lookup(pair, w0, tan_theta(v) * beta);    // uniform branch (a launch's parameter)
-    else g = epd_g1_lookup(g_epd_g1, p, tan_theta(v) * beta);
-#else
     const float g = epd_g1_lookup(g_epd_g1, p, tan_theta(v) * beta);
-#endif
     return mask ? g : 0.0f;
   }
 
@@ -265,10 +231,7 @@ struct VanGinneken
     auto phif = [](v3 v) { const float r = atan2f(v.y, v.x); return (r < 0) ? r + kPi2F : r; };
     const float phi = fabsf(phif(in) - phif(out));
 #endif
-    // float(4.41 phi / (4.41 phi + 1.0)) of doubles: f_div_d (an f32 reciprocal, one f64 remainder step: the double
-    // quotient to ~2^-46, so the same float except within that of a rounding midpoint) for the IEEE f64 division
-    const double lp = 4.41 * double(phi);
-    const float lambda = f_div_d(lp, lp + 1.0);
+    const float lambda = float(4.41 * double(phi) / (4.41 * double(phi) + 1.0));
     const float gi = ndf.G1(in, m), go = ndf.G1(out, m);
     const float gio = gi * go;
     const float maxg = fmaxf(gi, go), ming = fminf(gi, go);
@@ -310,14 +273,5 @@ using EpdM = Microfacet<EpdNdf, VanGinneken, FresnelComplex, Norm::Walter, false
 // Builds the G1 table on the current device once (inst_epd.hip) and points g_epd_g1 at it.
 int epd_prepare(hipStream_t s);
 template<> struct host_prepare<EpdM> { static int run(hipStream_t s) { return epd_prepare(s); } };
-
-// Per launch (eval / pdf / sample kernels): the two table rows the launch's p reads, interleaved (EpdNdf::G1), into
-// stream-ordered scratch; its address rides in the parameter block after the model's parameters.
-int epd_row_pair_run(ParamBlock& p, hipStream_t s, void** scratch);
-template<> struct host_params<EpdM>
-{
-  static int run(ParamBlock& p, uint32_t, hipStream_t s, void** scratch) { return epd_row_pair_run(p, s, scratch); }
-  static void done(void* scratch, hipStream_t s) { if (scratch) scratch_release(scratch, s); }
-};
 
 }  // namespace bbmhip

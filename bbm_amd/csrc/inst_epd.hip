@@ -181,41 +181,6 @@ int epd_prepare(hipStream_t s)
   return BBM_HIP_OK;
 }
 
-const float* epd_table_device(hipStream_t s);
-
-// The two rows of the table a launch with parameter p reads (core/precompute.h:126-198: floor / ceil of m0 = 5 / p - 1,
-// clamped), interleaved per column for EpdNdf::G1's single 16 B gather: pair[c] = (G1[f0][c], G1[c0][c], G1[f0][c'],
-// G1[c0][c']), c' = min(c + 1, 999).
-__global__ __launch_bounds__(256) void k_epd_row_pair(const float* __restrict__ tab, float p, float4* __restrict__ pair)
-{
-  math_tables_init();
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= kEpdCols) return;
-  const double m0 = 5.0 / double(p) - 1.0;
-  const int f0 = int(fmin(fmax(floor(m0), 0.0), double(kEpdRows - 1)));
-  const int c0 = int(fmin(fmax(ceil(m0), 0.0), double(kEpdRows - 1)));
-  const int cn = (c + 1 < kEpdCols) ? c + 1 : kEpdCols - 1;
-  pair[c] = make_float4(tab[f0 * kEpdCols + c], tab[c0 * kEpdCols + c], tab[f0 * kEpdCols + cn], tab[c0 * kEpdCols + cn]);
-}
-
-int epd_row_pair_run(ParamBlock& p, hipStream_t s, void** scratch)
-{
-  const float* tab = epd_table_device(s);
-  if (!tab) return fail(BBM_HIP_ERR_HIP, "EPD G1 table: not available on this device");
-  float4* pair = static_cast<float4*>(scratch_acquire(kEpdCols * sizeof(float4), s));
-  if (!pair) return fail(BBM_HIP_ERR_HIP, "EPD row pair: scratch allocation failed: " + scratch_failure());
-  hipLaunchKernelGGL(k_epd_row_pair, dim3((kEpdCols + 255) / 256), dim3(256), 0, s, tab, p.v[1], pair);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess)
-  {
-    scratch_release(pair, s);
-    return hip_fail(e, "row pair launch");
-  }
-  set_param_ptr(p.v, EpdNdf::kPairSlot, pair);
-  *scratch = pair;
-  return BBM_HIP_OK;
-}
-
 // Device address of the table on the current device (the doubleRGB EPD kernels, f64.hip, get it as a parameter)
 const float* epd_table_device(hipStream_t s)
 {

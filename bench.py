@@ -101,7 +101,8 @@ def cpu_baseline(model, din, dout, seconds):
     threads = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
     params = model.parameter_values()
     if ou.ref() is not None:
-        kind, fn = "reference", ou.ref_eval_pdf
+        kind = "reference"
+        fn = lambda *a, **k: ou._evalpdf(ou.ref_bench().bbmref_eval_pdf, *a[:4], 3, 0, k["nthreads"])   # noqa: E731
     else:
         kind, fn = "port", ou.port_eval_pdf
     fn(model.name, params, hin[:, :100_000], hout[:, :100_000], nthreads=threads)   # warm-up
@@ -115,7 +116,7 @@ def cpu_baseline(model, din, dout, seconds):
     return {"value": done / el, "unit": "pairs/s", "cores": threads, "kind": kind,
             "affinity_threads": aff, "physical_cores": phys, "smt_threads_per_core": smt, "cgroup_cpu_quota": quota,
             "sample": f"{n} pairs of the same synthetic batch, {done // n} passes in {el:.1f} s, "
-                      f"{model.name} eval+pdf via {'oracle/_ref (reference headers, native floatRGB)' if kind == 'reference' else 'oracle/port'}, "
+                      f"{model.name} eval+pdf via {'oracle/_ref (reference headers, native floatRGB, -O3 Release build)' if kind == 'reference' else 'oracle/port'}, "
                       f"OpenMP {threads} threads = every CPU this process may use (affinity mask: {aff} threads on "
                       f"{phys} physical cores x {smt} SMT{'' if quota is None else f'; cgroup CPU quota {quota:g} CPUs'}) "
                       f"on {cpu_model}"}
@@ -133,7 +134,7 @@ def lambertian_cpu(args):
     din = np.ascontiguousarray(ou.dirgen_numpy(SEED, 0, 0, n, mode=0))
     dout = np.ascontiguousarray(ou.dirgen_numpy(SEED, 1, 0, n, mode=0))
     params = np.array([0.5, 0.5, 0.5], np.float32)      # Lambertian's default albedo (lambertian.h:27)
-    lib, kind = ou.ref(), "reference"
+    lib, kind = ou.ref_bench(), "reference"
     if lib is None:
         lib, kind = ou.port(), "port"
         fn = lib.bbmport_eval_pdf

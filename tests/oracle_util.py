@@ -16,6 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 PORT_LIB = os.path.join(ROOT, "oracle", "_port", "libbbm_port.so")
 REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libbbm_ref.so")
+# the same shim built with the reference's Release flags (-O3, SLP vectorization on): timed by the cpu_baseline legs only
+REF_BENCH_LIB = os.path.join(ROOT, "oracle", "_ref", "libbbm_ref_bench.so")
 
 _libs = {}
 
@@ -40,6 +42,13 @@ def port():
 
 def ref():
     return _load(REF_LIB, "bbmref_")
+
+
+def ref_bench():
+    """The reference for CPU timing (bench.py / tools/bench_configs.py cpu_baseline): the -O3 Release build, or the
+    checker build where it is absent.  Never a checker: g++ 11.4's -O3 SLP miscompiles the He family's D
+    (oracle/Makefile, profiles/r06_oracle_slp.txt)."""
+    return _load(REF_BENCH_LIB, "bbmref_") or ref()
 
 
 def port_models():
@@ -544,10 +553,10 @@ def ref_loss_total(name, fitted, reference, grid, loss_kind):
     return np.float32(tot[0])
 
 
-def ref_pair_losses(name, fitted, reference, din, dout, loss_kind, nthreads=8):
+def ref_pair_losses(name, fitted, reference, din, dout, loss_kind, nthreads=8, lib=None):
     """Per-sample reference losses on explicit direction pairs (the reference's sampledlossfunction
     over a table linearizer, oracle/ref_fit.cpp): (n,) float32."""
-    lib = ref()
+    lib = lib or ref()
     din = np.ascontiguousarray(din, np.float32)
     dout = np.ascontiguousarray(dout, np.float32)
     n = din.shape[1]

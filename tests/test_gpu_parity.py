@@ -708,7 +708,7 @@ def test_bagher_out_of_range_parameters(bbm):
         params[3 * layout["alpha"]:3 * layout["alpha"] + 3] = alpha
         params[3 * layout["p"]:3 * layout["p"] + 3] = p
         m.set_parameter_values(params)
-        got = _gpu_evalpdf(m, din, dout, mode=1)[:3]
+        got = m.eval(_dev(din), _dev(dout)).cpu().numpy()
         ref = ou.oracle_eval_pdf("Bagher", params, din, dout, nthreads=8)[:3]
         same = (got == ref) | (np.isnan(got) & np.isnan(ref))
         ok = ou.parity_ok(got, ref) | same

@@ -138,7 +138,7 @@ def _cpu_lib():
     models it covers only)."""
     from tests import oracle_util as ou
     if ou.ref() is not None:
-        return ou.ref(), "reference"
+        return ou.ref_bench(), "reference"
     return None, "port"
 
 
@@ -258,7 +258,7 @@ def cpu_fit(name, fitted, reference, lin, seconds):
     hin, hout = din.cpu().numpy(), dout.cpu().numpy()
     fp = fitted.parameter_values()
     rp = reference.parameter_values()
-    calls, el = _timed_calls(lambda: ou.ref_pair_losses(name, fp, rp, hin, hout, 3, nthreads=threads), seconds)
+    calls, el = _timed_calls(lambda: ou.ref_pair_losses(name, fp, rp, hin, hout, 3, nthreads=threads, lib=lib), seconds)
     n = hin.shape[1]
     return {"value": calls * n / el, "unit": "probe-pairs/s", "cores": threads, "kind": kind,
             "sample": f"{calls} probes x the {n} MERL-grid pairs (standardLog), reference = the analytic fit "
