@@ -57,7 +57,12 @@ __device__ __forceinline__ float ndf_sampler_pdf(const float* __restrict__ cdf, 
   const int uidx = (ce < 0) ? kHeBins - 1 : min(int(ce), kHeBins - 1);
   auto cpdf = [&](int i) { return cdf[i] - ((i >= 1) ? cdf[i - 1] : 0.0f); };
   const float p = cpdf(lidx) * (1 - w) + cpdf(uidx) * w;
-  const float st = sqrtf(m.x * m.x + m.y * m.y);
+  // |sin(theta)| of the float theta as the reference takes it (bbm::sin -> glibc's sinf, restated: math.hpp) -- the
+  // direction's own sqrt(x^2 + y^2) (rounds 1-5) is the same quantity rounded differently, an ulp off on ~1/4 of the
+  // lanes, which moved the pdf by an ulp there
+  float sn, cs;
+  sincosf_glibc(theta, &sn, &cs);
+  const float st = __builtin_fabsf(sn);
   const float jac = (((sqrtf(theta) * kPiSqQuarterF) / float(kHeBins)) * st) * kPi2F;
   return ((m.z > 0) && (jac > kEpsF)) ? div_nr(p, jac) : 0.0f;
 }
