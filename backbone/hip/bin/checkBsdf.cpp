@@ -11,9 +11,9 @@
  *   rng=mt19937   the reference's own draw sequence -- one std::mt19937 seeded with `seed` and
  *                 uniform_real_distribution<float>(0, 1) per rndVec2d() (:21-26), consumed in the reference binary's
  *                 order -- with the per-sample BSDF calls batched on the GPU and every accumulation, check and printed
- *                 line on the host in the reference's loop order and float precision: test=reflectance and test=pdf
- *                 print what the reference prints for the same seed wherever the GPU's per-sample values are the
- *                 reference's floats (tests/test_gpu_cpp_cli.py diffs the two; oracle/ref_cli.cpp runs the reference).
+ *                 line on the host in the reference's loop order and float precision: every test prints what the
+ *                 reference prints for the same seed wherever the GPU's per-sample values are the reference's floats
+ *                 (tests/test_gpu_cpp_cli.py diffs the two; oracle/ref_cli.cpp runs the reference).
  * test=pdf runs the reference's loop in both modes (:219-243): it stops once `maxError` failures of one kind are
  * seen and prints each negative pdf and each sampled direction below the horizon as the reference does.
  * Built by tests/cpp/Makefile against the reference's headers (BBM_BACKBONE=hip) and libbbm_hip.so.
@@ -198,6 +198,198 @@ static void reflectanceOrdered(const hip::model_desc& m, size_t samples, size_t 
   }
 }
 
+// batched BSDF calls on host direction lists (one chunk), results back on the host
+static std::vector<Spectrum> evalBatch(const hip::model_desc& m, const std::vector<Vec3d>& in, const std::vector<Vec3d>& out,
+                                       unit_t unit)
+{
+  const size_t k = in.size();
+  dev3 di(k), dout(k), f(k);
+  di.upload(in);
+  dout.upload(out);
+  hip::eval(m, di.in(), dout.in(), k, f.out(), bsdf_flag::All, unit);
+  const auto v = f.download(k);
+  std::vector<Spectrum> r(k);
+  for(size_t j = 0; j < k; ++j) r[j] = Spectrum(v[j][0], v[j][1], v[j][2]);
+  return r;
+}
+
+static std::vector<float> pdfBatch(const hip::model_desc& m, const std::vector<Vec3d>& in, const std::vector<Vec3d>& out,
+                                   unit_t unit)
+{
+  const size_t k = in.size();
+  dev3 di(k), dout(k);
+  di.upload(in);
+  dout.upload(out);
+  hip::device_vector<float> p(k);
+  hip::pdf(m, di.in(), dout.in(), k, p.data(), bsdf_flag::All, unit);
+  return download(p, k);
+}
+
+// checkBsdf.cpp:102-140 / :145-185 in the reference's order (rng=mt19937): two sampleSphere directions per sample, the
+// evaluations batched, the float sums and the running maximum (first maximum kept on ties) on the host
+static void symmetryOrdered(const hip::model_desc& m, size_t samples, bool adjoint, draw_source& rng)
+{
+  Spectrum sum_r = 0, max_r = 0, sum_i = 0, max_i = 0;
+  Vec3dPair maxpair_r = {0, 0}, maxpair_i = {0, 0};
+  std::vector<float> x0[2], x1[2];
+  for(size_t s0 = 0; s0 < samples; s0 += kChunk)
+  {
+    const size_t k = std::min(kChunk, samples - s0);
+    rng.fill(s0, k, 2, x0, x1);
+    std::vector<Vec3d> a(k), b(k);
+    for(size_t j = 0; j < k; ++j)
+    {
+      a[j] = uniformDirection(Vec2d(x0[0][j], x1[0][j]), true).direction;
+      b[j] = uniformDirection(Vec2d(x0[1][j], x1[1][j]), true).direction;
+    }
+    const auto fr = evalBatch(m, a, b, unit_t::Radiance);
+    const auto br = evalBatch(m, b, a, adjoint ? unit_t::Importance : unit_t::Radiance);
+    std::vector<Spectrum> fi, bi;
+    if(!adjoint) { fi = evalBatch(m, a, b, unit_t::Importance); bi = evalBatch(m, b, a, unit_t::Importance); }
+    for(size_t j = 0; j < k; ++j)
+    {
+      const Vec3dPair dir = {a[j], b[j]};
+      Spectrum diff_r = bbm::abs(fr[j] - br[j]);
+      sum_r += diff_r;
+      if(bbm::any(bbm::hsum(diff_r) > bbm::hsum(max_r))) { maxpair_r = dir; max_r = diff_r; }
+      if(!adjoint)
+      {
+        Spectrum diff_i = bbm::abs(fi[j] - bi[j]);
+        sum_i += diff_i;
+        if(bbm::any(bbm::hsum(diff_i) > bbm::hsum(max_i))) { maxpair_i = dir; max_i = diff_i; }
+      }
+    }
+  }
+  sum_r /= samples;
+  if(adjoint)
+  {
+    std::cout << "Adjoint difference average = " << sum_r << ", max = " << max_r << " at " << maxpair_r << std::endl;
+    return;
+  }
+  sum_i /= samples;
+  std::cout << "Radiance   average = " << sum_r << ", max = " << max_r << " at " << maxpair_r << std::endl;
+  std::cout << "Importance average = " << sum_i << ", max = " << max_i << " at " << maxpair_i << std::endl;
+}
+
+// checkBsdf.cpp:250-290 in the reference's order (rng=mt19937): per trial its direction, then the sampleSphere draws
+static void pdfIntOrdered(const hip::model_desc& m, size_t samples, size_t trials, bool samplesphere, draw_source& rng)
+{
+  std::vector<float> x0[1], x1[1];
+  size_t off = 0;
+  for(size_t t = 0; t < trials; ++t)
+  {
+    Value pdf_r = 0, pdf_i = 0;
+    rng.fill(off++, 1, 1, x0, x1);
+    const BsdfSample sample_t = uniformDirection(Vec2d(x0[0][0], x1[0][0]), samplesphere);
+    for(size_t s0 = 0; s0 < samples; s0 += kChunk)
+    {
+      const size_t k = std::min(kChunk, samples - s0);
+      rng.fill(off, k, 1, x0, x1);
+      off += k;
+      std::vector<Vec3d> dirs(k), ts(k, sample_t.direction);
+      std::vector<Value> spdf(k);
+      for(size_t j = 0; j < k; ++j)
+      {
+        const BsdfSample u = uniformDirection(Vec2d(x0[0][j], x1[0][j]), true);
+        dirs[j] = u.direction;
+        spdf[j] = u.pdf;
+      }
+      const auto pr = pdfBatch(m, dirs, ts, unit_t::Radiance), pi = pdfBatch(m, dirs, ts, unit_t::Importance);
+      for(size_t j = 0; j < k; ++j)
+        if(bbm::any(spdf[j] > Constants::Epsilon()))
+        {
+          pdf_r += pr[j] / spdf[j];
+          pdf_i += pi[j] / spdf[j];
+        }
+    }
+    pdf_r /= samples;
+    pdf_i /= samples;
+    std::cout << " Integral = " << pdf_r << "/" << pdf_i << " (radiance/importance) for " << sample_t.direction << std::endl;
+  }
+}
+
+// checkBsdf.cpp:300-418 in the reference's order (rng=mt19937): per trial its direction, the per-bin pdf integrals
+// (bin by bin, pdfSamples draws each), then the sample counts, the chi-square and P as the reference forms them
+static void sampleOrdered(const hip::model_desc& m, size_t pdfSamples, size_t samples, size_t theta, size_t phi,
+                          size_t trials, bool samplesphere, bool includeZeroPdfSamples, draw_source& rng)
+{
+  std::vector<float> x0[1], x1[1];
+  size_t off = 0;
+  for(size_t tr = 0; tr < trials; ++tr)
+  {
+    rng.fill(off++, 1, 1, x0, x1);
+    const BsdfSample sample_t = uniformDirection(Vec2d(x0[0][0], x1[0][0]), samplesphere);
+    std::vector<Value> pdf(theta * phi, 0), count(theta * phi, 0);
+    // the pdf integrals: all bins' draws in order, evaluated in chunks
+    const size_t total = theta * phi * pdfSamples;
+    Vec2d sph_coord;
+    for(size_t s0 = 0; s0 < total; s0 += kChunk)
+    {
+      const size_t k = std::min(kChunk, total - s0);
+      rng.fill(off, k, 1, x0, x1);
+      off += k;
+      std::vector<Vec3d> dirs(k), ts(k, sample_t.direction);
+      std::vector<Value> w(k);
+      for(size_t j = 0; j < k; ++j)
+      {
+        const size_t idx = (s0 + j) / pdfSamples, t = idx / phi, p = idx % phi;
+        const Vec2d rnd(x0[0][j], x1[0][j]);
+        spherical::phi(sph_coord) = Constants::Pi(2) * (p + rnd[0]) / phi;
+        spherical::theta(sph_coord) = Constants::Pi() * (t + rnd[1]) / theta;
+        dirs[j] = spherical::convert(sph_coord);
+        w[j] = Constants::Pi2(2) * bbm::abs(spherical::sinTheta(sph_coord)) / (phi * theta);
+      }
+      const auto pv = pdfBatch(m, dirs, ts, unit_t::Radiance);
+      for(size_t j = 0; j < k; ++j)
+      {
+        const size_t idx = (s0 + j) / pdfSamples;
+        pdf[idx] += pv[j] * w[j];
+        if((s0 + j) % pdfSamples == pdfSamples - 1) pdf[idx] /= pdfSamples;
+      }
+    }
+    // the sample counts
+    for(size_t s0 = 0; s0 < samples; s0 += kChunk)
+    {
+      const size_t k = std::min(kChunk, samples - s0);
+      rng.fill(off, k, 1, x0, x1);
+      off += k;
+      dev3 dt(k), dd(k);
+      dt.upload(std::vector<Vec3d>(k, sample_t.direction));
+      hip::device_vector<float> a(k), b(k), sp(k);
+      hip::device_vector<uint32_t> fl(k);
+      upload_of(a, x0[0]); upload_of(b, x1[0]);
+      hip::sample(m, dt.in(), a.data(), b.data(), k, dd.out(), sp.data(), fl.data());
+      const auto dirs = dd.download(k);
+      const auto hp = download(sp, k);
+      for(size_t j = 0; j < k; ++j)
+        if(includeZeroPdfSamples || bbm::any(hp[j] > Constants::Epsilon()))
+        {
+          sph_coord = spherical::convert(dirs[j]);
+          size_t t = bbm::cast<size_t>(bbm::min(spherical::theta(sph_coord) / Constants::Pi() * theta, theta - 1));
+          size_t p = bbm::cast<size_t>(bbm::min(spherical::phi(sph_coord) / Constants::Pi(2) * phi, phi - 1));
+          count[t * phi + p]++;
+        }
+    }
+    Value chi2 = 0, df = -1;
+    for(size_t idx = 0; idx < theta * phi; ++idx)
+    {
+      Value mm = pdf[idx] * samples;
+      if(bbm::any(mm > Constants::Epsilon() && count[idx] > 5))
+      {
+        chi2 += pow(count[idx] - mm, 2) / mm;
+        df++;
+      }
+    }
+    std::cout << " Chi2 for " << sample_t.direction << " = " << chi2 << " (with " << df << " degrees of freedom)." << std::endl;
+    if(bbm::any(df > 1))
+    {
+      Value P = bbm::gamma_q((df - 1) / 2, chi2 / 2);
+      std::cout << "  P = " << P << " (reject if lower than confidence)." << std::endl;
+    }
+    else std::cout << " No degrees of freedom; need at least 1 to compute P." << std::endl;
+  }
+}
+
 static void testReflectance(const hip::model_desc& m, const option_parser& opt, uint64_t seed)
 {
   size_t samples = opt.get<size_t>("samples", 100000);
@@ -221,6 +413,12 @@ static void testReciprocity(const hip::model_desc& m, const option_parser& opt, 
   size_t samples = opt.get<size_t>("samples", 1000000);
   if(!valid(opt, {"bsdfmodel", "test", "samples"})) return;
   std::cout << "Reciprocity test with " << samples << " samples." << std::endl;
+  if(opt.get<std::string>("rng", "counter") == "mt19937")
+  {
+    draw_source rng(true, seed, BBM_CHECK_RECIPROCITY);
+    symmetryOrdered(m, samples, false, rng);
+    return;
+  }
   const auto r = hip::check_reciprocity(m, samples, seed);
   const Vec3dPair pr{to_vec(r[0].in), to_vec(r[0].out)}, pi{to_vec(r[1].in), to_vec(r[1].out)};
   std::cout << "Radiance   average = " << spec(r[0].average) << ", max = " << spec(r[0].max) << " at " << pr << std::endl;
@@ -232,6 +430,12 @@ static void testAdjoint(const hip::model_desc& m, const option_parser& opt, uint
   size_t samples = opt.get<size_t>("samples", 100000);
   if(!valid(opt, {"bsdfmodel", "test", "samples"})) return;
   std::cout << "Adjoint test with " << samples << " samples." << std::endl;
+  if(opt.get<std::string>("rng", "counter") == "mt19937")
+  {
+    draw_source rng(true, seed, BBM_CHECK_ADJOINT);
+    symmetryOrdered(m, samples, true, rng);
+    return;
+  }
   const auto r = hip::check_adjoint(m, samples, seed);
   const Vec3dPair pa{to_vec(r.in), to_vec(r.out)};
   std::cout << "Adjoint difference average = " << spec(r.average) << ", max = " << spec(r.max) << " at " << pa << std::endl;
@@ -298,6 +502,12 @@ static void testPdfInt(const hip::model_desc& m, const option_parser& opt, uint6
   if(!valid(opt, {"bsdfmodel", "test", "samples", "trials", "sampleSphere"})) return;
   std::cout << "Tesing PDF Integral with " << samples << " samples, for " << trials << " random directions sampled over the "
             << ((samplesphere) ? "sphere" : "hemisphere") << std::endl;
+  if(opt.get<std::string>("rng", "counter") == "mt19937")
+  {
+    draw_source rng(true, seed, BBM_CHECK_PDFINT);
+    pdfIntOrdered(m, samples, trials, samplesphere, rng);
+    return;
+  }
   const auto r = hip::check_pdf_int(m, samples, trials, samplesphere, seed);
   for(size_t t = 0; t < trials; ++t)
     std::cout << " Integral = " << Value(r.integral[t][0]) << "/" << Value(r.integral[t][1]) << " (radiance/importance) for "
@@ -318,6 +528,12 @@ static void testSample(const hip::model_desc& m, const option_parser& opt, uint6
             << " direction samples, with (" << phi << " x " << theta << ") bins over " << trials << " trials";
   if(includeZeroPdfSamples) std::cout << ", including zero pdf samples";
   std::cout << "." << std::endl;
+  if(opt.get<std::string>("rng", "counter") == "mt19937")
+  {
+    draw_source rng(true, seed, BBM_CHECK_SAMPLE_PDF);
+    sampleOrdered(m, pdfSamples, samples, theta, phi, trials, samplesphere, includeZeroPdfSamples, rng);
+    return;
+  }
   const auto r = hip::check_sample(m, pdfSamples, samples, theta, phi, trials, samplesphere, includeZeroPdfSamples, seed);
   for(const auto& t : r)
   {
@@ -338,7 +554,7 @@ int main(int argc, char** argv)
     std::cout << "  + test=pdf [samples=100000] [maxError=10] [checkBelowHorizon] [sampleSphere]: checks if the PDF >= 0, and the PDF returned by the sampling method matches the pdf from the pdf-method. Abort if the number of fails exceeds 'maxError'" << std::endl;
     std::cout << "  + test=pdfInt [samples=100000] [trials=10] [sampleSphere]: checks the integral (MC with 'samples' samples) of the PDF for 'trials' different directions." << std::endl;
     std::cout << "  + test=sample [pdfSamples=4069] [samples=100000] [theta=10] [phi=20] [trials=10] [sampleSphere] [includeZeroPdfSamples]: perform Chi2 test on the sample vs the pdf method.  The domain is subdivided in [theta x phi] bins, and for each bin we integrate the PDF using MC.  A higher sampling rate might be needed for sharp BSDFs." << std::endl;
-    std::cout << "  (HIP backbone) [seed=5489] [rng=counter|mt19937]: the draws' seed; the library's counter draws (GPU reductions) or the reference's std::mt19937 sequence (reflectance, pdf)." << std::endl;
+    std::cout << "  (HIP backbone) [seed=5489] [rng=counter|mt19937]: the draws' seed; the library's counter draws (GPU reductions) or the reference's std::mt19937 sequence and loop order." << std::endl;
     return -1;
   }
   try

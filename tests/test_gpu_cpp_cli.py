@@ -121,14 +121,17 @@ def test_cli_options_follow_reference(bbm):
     assert r.returncode != 0 and "ERROR" in r.stdout
 
 
-def _cli_oracle(tree, test, samples, a, flag0, flag1, seed=5489):
-    """The reference's own checkBsdf test loop (oracle/ref_cli.cpp) on the reference's bsdf_ptr: printed text."""
+def _cli_oracle(tree, test, opts, seed=5489):
+    """The reference's own checkBsdf test loop (oracle/ref_cli.cpp) on the reference's bsdf_ptr: printed text.
+    test: 0 reflectance, 1 pdf, 2 reciprocity, 3 adjoint, 4 pdfInt, 5 sample; opts as bbmref_cli_test documents."""
     import ctypes
     lib = ou.ref()
     k, names, nk, params, nps = ou.runtime_tree(tree)
+    o = np.zeros(8, np.uint64)
+    o[:len(opts)] = opts
     buf = ctypes.create_string_buffer(1 << 20)
-    n = lib.bbmref_cli_test(k, names, nk, params.ctypes.data_as(ctypes.c_void_p), nps, test, ctypes.c_size_t(samples),
-                            ctypes.c_size_t(a), flag0, flag1, ctypes.c_uint64(seed), buf, len(buf))
+    n = lib.bbmref_cli_test(k, names, nk, params.ctypes.data_as(ctypes.c_void_p), nps, test,
+                            o.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint64(seed), buf, len(buf))
     assert 0 <= n < len(buf)
     return buf.value.decode()
 
@@ -149,30 +152,38 @@ def _diff_cli(got, want):
     return same
 
 
-@pytest.mark.parametrize("case", ["pdf_ct_below", "pdf_lambertian_sphere", "refl_lambertian", "refl_ct_importance"])
+CT = ("CookTorrance", [0.5, 0.5, 0.5, 0.3, 1.3])
+LAMB = ("Lambertian", [0.5, 0.5, 0.5])
+WARD = ("Ward", [0.5, 0.5, 0.5, 0.3, 0.2])
+CLI_CASES = {
+    # grazing uniform directions: microfacet reflection sends some samples below the horizon; maxError = 4 stops the
+    # loop at the 4th of one kind, after printing each
+    "pdf_ct_below": (["bsdfmodel=CookTorrance(roughness=0.5)", "test=pdf", "samples=20000", "maxError=4",
+                      "checkBelowHorizon"], ("CookTorrance", [0.5, 0.5, 0.5, 0.5, 1.3]), 1, [20000, 4, 1, 0]),
+    "pdf_lambertian_sphere": (["bsdfmodel=Lambertian", "test=pdf", "samples=30000", "sampleSphere", "checkBelowHorizon"],
+                              LAMB, 1, [30000, 10, 1, 1]),
+    "refl_lambertian": (["bsdfmodel=Lambertian", "test=reflectance", "samples=40000", "theta=3"], LAMB, 0, [40000, 3, 0]),
+    "refl_ct_importance": (["bsdfmodel=CookTorrance(roughness=0.3)", "test=reflectance", "samples=40000", "theta=2",
+                            "importanceSampling"], CT, 0, [40000, 2, 1]),
+    "reciprocity_ward": (["bsdfmodel=Ward(roughness=[0.3,0.2])", "test=reciprocity", "samples=30000"], WARD, 2, [30000]),
+    "adjoint_ct": (["bsdfmodel=CookTorrance(roughness=0.3)", "test=adjoint", "samples=30000"], CT, 3, [30000]),
+    "pdfint_ct": (["bsdfmodel=CookTorrance(roughness=0.3)", "test=pdfInt", "samples=20000", "trials=3"], CT, 4,
+                  [20000, 3, 0]),
+    "sample_ct": (["bsdfmodel=CookTorrance(roughness=0.3)", "test=sample", "pdfSamples=64", "samples=20000", "theta=5",
+                   "phi=8", "trials=2"], CT, 5, [64, 20000, 5, 8, 2, 0, 0]),
+}
+
+
+@pytest.mark.parametrize("case", list(CLI_CASES))
 def test_cli_mt19937_matches_reference(bbm, case):
     """rng=mt19937: the CLI consumes the reference's std::mt19937 draw sequence and runs the reference's loop order,
     so its printed lines are the reference's (oracle/ref_cli.cpp runs the reference's test on the reference's
     bsdf_ptr with the same seed): the same lines -- the pdf test's per-failure lines and its stop at maxError
-    included -- and the same numbers."""
+    included -- and the same numbers, for every checkBsdf test."""
     seed = 1234
-    if case == "pdf_ct_below":
-        # grazing uniform directions: microfacet reflection sends some samples below the horizon; maxError = 4 stops
-        # the loop at the 4th of one kind, after printing each
-        args = ["bsdfmodel=CookTorrance(roughness=0.5)", "test=pdf", "samples=20000", "maxError=4", "checkBelowHorizon"]
-        tree, want = ("CookTorrance", [0.5, 0.5, 0.5, 0.5, 1.3]), (1, 20000, 4, 1, 0)
-    elif case == "pdf_lambertian_sphere":
-        args = ["bsdfmodel=Lambertian", "test=pdf", "samples=30000", "sampleSphere", "checkBelowHorizon"]
-        tree, want = ("Lambertian", [0.5, 0.5, 0.5]), (1, 30000, 10, 1, 1)
-    elif case == "refl_lambertian":
-        args = ["bsdfmodel=Lambertian", "test=reflectance", "samples=40000", "theta=3"]
-        tree, want = ("Lambertian", [0.5, 0.5, 0.5]), (0, 40000, 3, 0, 0)
-    else:
-        args = ["bsdfmodel=CookTorrance(roughness=0.3)", "test=reflectance", "samples=40000", "theta=2",
-                "importanceSampling"]
-        tree, want = ("CookTorrance", [0.5, 0.5, 0.5, 0.3, 1.3]), (0, 40000, 2, 1, 0)
+    args, tree, test, opts = CLI_CASES[case]
     got = _run(*args, "rng=mt19937", f"seed={seed}")
-    ref = _cli_oracle(tree, *want, seed=seed)
+    ref = _cli_oracle(tree, test, opts, seed=seed)
     same = _diff_cli(got, ref)
     print(f"{case}: {same} of {len(ref.strip().splitlines())} lines identical\n{got}")
     if case == "pdf_ct_below":
