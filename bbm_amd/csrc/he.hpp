@@ -165,14 +165,32 @@ struct He
   // lobe is 0/0 (NaN) in the reference, and so is this one, but a masked lane is select(mask, ., 0) there.
   __device__ __forceinline__ bool masked(uint32_t component) const { return component != launch_component; }
 
-  // S1 (he.h:266-291), Eqs. 24-25
-  __device__ __forceinline__ float S1(v3 v) const
+  // The four erfcf evaluations of a pair's prelude -- S1 of in and out, sigma's K of in and out -- are 40 % of the
+  // prelude (0.16 of 0.36 ms per 10 M He pairs, profiles/r06_ab_he_erfc.txt): each one a three-range fdlibm
+  // erfcf whose ranges diverge within every wave.  Their arguments (erfc_args) are therefore separable from the
+  // rest: the compaction kernel (kernels.hpp) evaluates a block's arguments as one work list sorted by range, S1's
+  // and K's argument of a direction evaluated once where they are the same float, and hands the values back
+  // (Erfc); every other path passes none and evaluates them in place.  Same function, same operands: same floats.
+  static constexpr bool kErfcList = true;
+  struct Erfc { float x[2], v[4]; };          // x: S1's arguments (in, out); v: erfcf of the four arguments
+  __device__ __forceinline__ float s1_arg(v3 v) const
+  {
+    const float cot = div_nr(1.0f, tan_theta(v));
+    // the double quotient stored straight into a float: f_div_d rounds like the reference
+    return f_div_d(double(tau * cot), 2.0 * double(sigma0));
+  }
+  __device__ __forceinline__ float k_arg(float t) const { return div_nr(tau, 2 * sigma0 * t); }
+  __device__ __forceinline__ void erfc_args(v3 in, v3 out, float* x) const
+  {
+    x[0] = s1_arg(in); x[1] = s1_arg(out);
+    x[2] = k_arg(tan_theta(in)); x[3] = k_arg(tan_theta(out));
+  }
+  // S1 (he.h:266-291), Eqs. 24-25, of a direction whose s1_arg is scot and erfcf(scot) = ec
+  __device__ __forceinline__ float S1(float scot, float ec) const
   {
     const bool smooth = sigma0 < kEpsF;
-    const float cot = div_nr(1.0f, tan_theta(v));
+    const float erfc_ = 0.5f * ec;                  // float(0.5 * double(e)): exact; glibc's erfcf, bit for bit
     // the double quotients below are stored straight into floats: f_div_d rounds like the reference
-    const float scot = f_div_d(double(tau * cot), 2.0 * double(sigma0));
-    const float erfc_ = 0.5f * erfcf_glibc(scot);   // float(0.5 * double(e)): exact; glibc's erfcf, bit for bit
     float lambda = f_div_d(0.5 * double(kInvSqrtPiF), double(scot));
     // Lambda *= exp(-pow(scot, 2.0)): a float times the double exponential, rounded once (compound assignment of a
     // double to a float); exp_dd is within ~2^-44 of glibc's exp, so the product rounds like the reference's
@@ -181,6 +199,7 @@ struct He
     const float S = f_div_d(1.0 - double(erfc_), double(lambda) + 1.0);
     return smooth ? 1.0f : S;
   }
+  __device__ __forceinline__ float S1(v3 v) const { const float x = s1_arg(v); return S1(x, erfcf_glibc(x)); }
 
   // G (he.h:306-352), Eq. 76
   __device__ __forceinline__ float G(v3 in, v3 out) const
@@ -203,13 +222,13 @@ struct He
     return (denom > kEpsF) ? g : 1.0f;
   }
 
-  // sigma (he.h:365-400), Eq. 80 by 4 Newton-Raphson steps
-  __device__ __forceinline__ float sigma(v3 in, v3 out) const
+  // sigma (he.h:365-400), Eq. 80 by 4 Newton-Raphson steps; K's erfcf from the work list (ef) or in place
+  __device__ __forceinline__ float sigma(v3 in, v3 out, const Erfc* ef) const
   {
     const float ti = tan_theta(in), to = tan_theta(out);
-    auto K = [&](float t) { return t * erfcf_glibc(div_nr(tau, 2 * sigma0 * t)); };
-    const float Ki = (ti > kEpsF) ? K(ti) : 0.0f;
-    const float Ko = (to > kEpsF) ? K(to) : 0.0f;
+    auto K = [&](float t, int k) { return t * (ef ? ef->v[k] : erfcf_glibc(k_arg(t))); };
+    const float Ki = (ti > kEpsF) ? K(ti, 2) : 0.0f;
+    const float Ko = (to > kEpsF) ? K(to, 3) : 0.0f;
     const float f0 = div_nr(1.0f, sqrtf(kPi8F)) * (Ki + Ko);
     // safe_sqrt(2.0 * log(f0)): 2 x a float is exact in float and double alike, and a correctly rounded double
     // sqrt rounded to float is the correctly rounded float sqrt (53 >= 2 x 24 + 2): identical, without the f64 sqrt
@@ -235,10 +254,10 @@ struct He
   // and the blend; D = both, in order, so every path evaluates the same operations on the same operands.
   struct DPrep { float gg[3], eb[3], rough[3]; };
 
-  __device__ __forceinline__ void D_prep(v3 in, v3 out, DPrep& d) const
+  __device__ __forceinline__ void D_prep(v3 in, v3 out, const Erfc* ef, DPrep& d) const
   {
     const float vxy2 = sqnorm2(in.x + out.x, in.y + out.y);
-    const float sg = sigma(in, out);
+    const float sg = sigma(in, out, ef);
     const float tau2 = float(double(tau) * double(tau));
     const float base = (vxy2 * tau2) / 4.0f;
     double g[3];
@@ -426,7 +445,7 @@ struct He
   __device__ __forceinline__ void D(v3 in, v3 out, float* Dout) const
   {
     DPrep d;
-    D_prep(in, out, d);
+    D_prep(in, out, nullptr, d);
     D_series(d, Dout);
   }
 
@@ -437,13 +456,13 @@ struct He
   // product.
   struct EvalPrep { float pre[3]; bool active; DPrep d; };
 
-  __device__ __forceinline__ void eval_prep(v3 in, v3 out, uint32_t component, EvalPrep& e) const
+  __device__ __forceinline__ void eval_prep(v3 in, v3 out, uint32_t component, const Erfc* ef, EvalPrep& e) const
   {
     e.active = (component & kFlagSpecular) && (in.z > 0) && (out.z > 0);
     float F[3];
-    const float S = S1(in) * S1(out);
+    const float S = ef ? S1(ef->x[0], ef->v[0]) * S1(ef->x[1], ef->v[1]) : S1(in) * S1(out);
     const float Gv = G(in, out);
-    D_prep(in, out, e.d);
+    D_prep(in, out, ef, e.d);
     // float(safe_sqrt(double(1 + dot) / 2.0)): halving the float sum is exact in float (1 + dot >= 2^-24 or 0),
     // and the double-then-float sqrt equals the float sqrt (53 >= 2 x 24 + 2)
     const float cth = safe_sqrtf((1 + dot3(in, out)) * 0.5f);
@@ -452,7 +471,7 @@ struct He
 #pragma unroll
     for (int c = 0; c < 3; ++c) e.pre[c] = ((nrm * F[c]) * S) * Gv;
 #if defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG == 2
-    e.pre[0] = sigma(in, out); e.pre[1] = S; e.pre[2] = Gv;
+    e.pre[0] = sigma(in, out, ef); e.pre[1] = S; e.pre[2] = Gv;
 #elif defined(BBM_HIP_HE_DIAG) && BBM_HIP_HE_DIAG == 3
     e.pre[0] = F[0]; e.pre[1] = F[1]; e.pre[2] = nrm;
 #endif
@@ -484,7 +503,7 @@ struct He
   __device__ __forceinline__ void eval_rgb(v3 in, v3 out, uint32_t component, float* rgb) const
   {
     EvalPrep e;
-    eval_prep(in, out, component, e);
+    eval_prep(in, out, component, nullptr, e);
     eval_finish<SCALE>(e, rgb);
   }
 
@@ -545,9 +564,9 @@ struct He
     st.pdf = base[13 * stride];
   }
   template<int MODE>
-  __device__ __forceinline__ int stage1(v3 in, v3 out, uint32_t component, Stage& st) const
+  __device__ __forceinline__ int stage1(v3 in, v3 out, uint32_t component, const Erfc* ef, Stage& st) const
   {
-    eval_prep(in, out, component, st.e);
+    eval_prep(in, out, component, ef, st.e);
     st.pdf = (MODE & kModePdf) ? pdf_of(in, out, component) : 0.0f;
     return D_key(st.e.d);
   }

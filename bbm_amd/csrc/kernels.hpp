@@ -148,7 +148,12 @@ __device__ __forceinline__ float4 ld4(const float* p, uint64_t t)
 template<bool NT>
 __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, float c, float d)
 {
-  if (NT) __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
+#ifdef BBM_HIP_PLAIN_STORES
+  if (false)           // A/B: nontemporal loads with plain stores
+#else
+  if (NT)
+#endif
+    __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
   else reinterpret_cast<float4*>(p)[t] = make_float4(a, b, c, d);
 }
 
@@ -439,6 +444,101 @@ template<class Model> constexpr int stage_words()
   else return 1;
 }
 
+// Models whose two-phase prelude hands a few libm evaluations to a block-wide work list (He: its four erfcf,
+// he.hpp kErfcList): each thread's arguments go into LDS sorted by the function's argument range (fdlibm's erfcf
+// runs one of three code paths per range, and a wave whose lanes span all three runs all three), then the block
+// evaluates the list densely -- every wave but the ones at a range boundary runs a single path -- and each thread
+// reads its values back.  S1's and K's argument of a direction are often the same float: evaluated once.  Same
+// function on the same operands as the inline evaluation: the same floats.
+template<class Model> constexpr bool erfc_list()
+{
+  if constexpr (requires { Model::kErfcList; }) return Model::kErfcList;
+  else return false;
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t mask)
+{
+  return int(__builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u)));
+}
+
+// All kBlock threads call this (block barriers inside).  list: >= 4 * kBlock floats of LDS, free until the call
+// returns; cnt: per-wave range counts.
+template<class Model>
+__device__ __forceinline__ void erfc_block(const Model& m, bool mine, v3 in, v3 out, typename Model::Erfc& ef,
+                                           float* list, int (*cnt)[4])
+{
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float x[4];
+  m.erfc_args(in, out, x);
+  ef.x[0] = x[0];
+  ef.x[1] = x[1];
+  // K's argument equal to S1's of the same direction: one evaluation serves both
+  const bool dup2 = __float_as_uint(x[2]) == __float_as_uint(x[0]);
+  const bool dup3 = __float_as_uint(x[3]) == __float_as_uint(x[1]);
+  int r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = mine ? erfcf_range(x[k]) : 0;    // 0: no list entry (range 0 is inline)
+  r[2] = dup2 ? 0 : r[2];
+  r[3] = dup3 ? 0 : r[3];
+  uint64_t bal[4][3];
+  int wc[3] = {0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      bal[k][c] = __builtin_amdgcn_ballot_w64(r[k] == c + 1);
+      wc[c] += __builtin_popcountll(bal[k][c]);
+    }
+  if (lane == 0)
+    for (int c = 0; c < 3; ++c) cnt[wave][c] = wc[c];
+  __syncthreads();
+  int start[3], before[3], end[3];
+  int run = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+  {
+    start[c] = run;
+    before[c] = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w)
+    {
+      const int v = cnt[w][c];
+      before[c] += (w < wave) ? v : 0;
+      run += v;
+    }
+    end[c] = run;
+  }
+  int pos[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+  {
+    pos[k] = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      if (r[k] == c + 1) pos[k] = start[c] + before[c] + lanes_below(bal[k][c]);
+      before[c] += __builtin_popcountll(bal[k][c]);
+    }
+    if (r[k] != 0) list[pos[k]] = x[k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < end[2]; e += kBlock)
+  {
+    const float xv = list[e];
+    float v;
+    if (e < end[0]) v = erfcf_r1(xv);
+    else if (e < end[1]) v = erfcf_r2(xv);
+    else v = erfcf_r3(xv);
+    list[e] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ef.v[k] = (r[k] != 0) ? list[pos[k]] : erfcf_r0(x[k]);
+  ef.v[2] = dup2 ? ef.v[0] : ef.v[2];
+  ef.v[3] = dup3 ? ef.v[1] : ef.v[3];
+}
+
 template<class Model, int MODE, bool MASK>
 __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compact(EvalArgs a)
 {
@@ -450,6 +550,7 @@ __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compac
   __shared__ float stage[two_phase<Model, MODE>() ? stage_words<Model>() : 1][kBlock];
   __shared__ short origin[kBlock];
   __shared__ int bucket[kSortBuckets], bucket_off[kSortBuckets];
+  __shared__ int erfc_cnt[erfc_list<Model>() ? kBlock / 64 : 1][4];
   const Model m(a.p.v);
   const uint64_t n4 = a.n >> 2;
   const uint64_t tiles = (n4 + kBlock - 1) / kBlock;
@@ -520,9 +621,16 @@ __global__ __launch_bounds__(kBlock) BBM_HIP_COMPACT_ATTR void k_eval_pdf_compac
         const bool mine = q < total;
         typename Model::Stage st;
         int key = 0;
-        if (mine)
-          key = m.template stage1<MODE>(mk3(job[0][q], job[1][q], job[2][q]), mk3(job[3][q], job[4][q], job[5][q]),
-                                        a.component, st);
+        const v3 jin = mk3(job[0][q], job[1][q], job[2][q]), jout = mk3(job[3][q], job[4][q], job[5][q]);
+        if constexpr (erfc_list<Model>())
+        {
+          // the stage rows are free until the bucket sort below: the erfc work list's LDS
+          static_assert(stage_words<Model>() >= 4, "the erfc work list needs 4 floats per thread");
+          typename Model::Erfc ef;
+          erfc_block(m, mine, jin, jout, ef, &stage[0][0], erfc_cnt);
+          if (mine) key = m.template stage1<MODE>(jin, jout, a.component, &ef, st);
+        }
+        else if (mine) key = m.template stage1<MODE>(jin, jout, a.component, nullptr, st);
         if (threadIdx.x < kSortBuckets) bucket[threadIdx.x] = 0;
         __syncthreads();
         const int rank = mine ? atomicAdd(&bucket[key], 1) : 0;

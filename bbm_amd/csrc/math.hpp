@@ -638,34 +638,50 @@ __device__ __forceinline__ float tail_r(float ax, uint32_t split, uint32_t mask)
 }
 }  // namespace fdlibm_erf
 
-__device__ __forceinline__ float erfcf_glibc(float x)
+// erfcf's three argument ranges as separate pieces (erfcf_glibc below is their composition; the He family's
+// compaction kernel sorts the arguments of a block by range and evaluates each range densely, he.hpp):
+// range of x: 0 = |x| >= 28, NaN (no arithmetic), 1 = |x| < 0.84375, 2 = [0.84375, 1.25), 3 = [1.25, 28)
+__device__ __forceinline__ int erfcf_range(float x)
+{
+  const uint32_t ix = __float_as_uint(x) & 0x7fffffffu;
+  return (ix < 0x3f580000u) ? 1 : ((ix < 0x3fa00000u) ? 2 : ((ix < 0x41e00000u) ? 3 : 0));
+}
+__device__ __forceinline__ float erfcf_r0(float x) { return (x != x) ? x : ((__float_as_uint(x) >> 31) ? 2.0f : 0.0f); }
+__device__ __forceinline__ float erfcf_r1(float x)
 {
   using namespace fdlibm_erf;
   const uint32_t hx = __float_as_uint(x), ix = hx & 0x7fffffffu;
-  const bool neg = (hx >> 31) != 0;
+  const float y = small_y(x);
+  float r = x * y;
+  r += (x - 0.5f);
+  const float res = (int32_t(hx) < 0x3e800000) ? 1.0f - (x + x * y) : 0.5f - r;
+  return (ix < 0x32800000u) ? 1.0f - x : res;
+}
+__device__ __forceinline__ float erfcf_r2(float x)
+{
+  using namespace fdlibm_erf;
+  const float pq = mid_pq(__builtin_fabsf(x));
+  return (__float_as_uint(x) >> 31) ? 1.0f + (erx + pq) : (1.0f - erx) - pq;
+}
+__device__ __forceinline__ float erfcf_r3(float x)
+{
+  using namespace fdlibm_erf;
+  const uint32_t ix = __float_as_uint(x) & 0x7fffffffu;
   const float ax = __builtin_fabsf(x);
+  // r / x can fall to ~1e-37 (x ~ 9): the f64 remainder step (div_sub<true>) keeps that quotient exact where
+  // div_nr's f32 remainder would be subnormal
+  const float q = div_sub<true>(tail_r(ax, 0x4036DB6Du, 0xffffe000u), ax);
+  return (__float_as_uint(x) >> 31) ? ((ix >= 0x40c00000u) ? 2.0f : 2.0f - q) : q;    // x < -6: 2 - tiny = 2
+}
+
+__device__ __forceinline__ float erfcf_glibc(float x)
+{
+  const uint32_t ix = __float_as_uint(x) & 0x7fffffffu;
   float res;
-  if (ix < 0x3f580000u)
-  {
-    const float y = small_y(x);
-    float r = x * y;
-    r += (x - 0.5f);
-    res = (int32_t(hx) < 0x3e800000) ? 1.0f - (x + x * y) : 0.5f - r;
-    res = (ix < 0x32800000u) ? 1.0f - x : res;
-  }
-  else if (ix < 0x3fa00000u)
-  {
-    const float pq = mid_pq(ax);
-    res = neg ? 1.0f + (erx + pq) : (1.0f - erx) - pq;
-  }
-  else if (ix < 0x41e00000u)
-  {
-    // r / x can fall to ~1e-37 (x ~ 9): the f64 remainder step (div_sub<true>) keeps that quotient exact where
-    // div_nr's f32 remainder would be subnormal
-    const float q = div_sub<true>(tail_r(ax, 0x4036DB6Du, 0xffffe000u), ax);
-    res = neg ? ((ix >= 0x40c00000u) ? 2.0f : 2.0f - q) : q;    // x < -6: 2 - tiny = 2
-  }
-  else res = neg ? 2.0f : 0.0f;                                // |x| >= 28 (inf included): 2 - tiny, tiny^2
+  if (ix < 0x3f580000u) res = erfcf_r1(x);
+  else if (ix < 0x3fa00000u) res = erfcf_r2(x);
+  else if (ix < 0x41e00000u) res = erfcf_r3(x);
+  else res = erfcf_r0(x);                                      // |x| >= 28 (inf included): 2 - tiny, tiny^2
   return (x != x) ? x : res;
 }
 

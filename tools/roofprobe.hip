@@ -6,6 +6,8 @@
 //   variant 1: nontemporal loads and stores
 //   variant 2: 8 pairs per thread-iteration (two float4 per stream in flight)
 //   variant 3: read-only (6 streams), variant 4: write-only (4 streams)
+//   variant 15: nontemporal loads, plain stores; variant 16: plain loads, nontemporal stores (the read-only and
+//               write-only calibrations favour nt for reads and plain for writes)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -210,6 +212,26 @@ __global__ __launch_bounds__(256) void k_probe_aos(Args a)
   }
 }
 
+template<bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_probe_mix(Args a)
+{
+  const uint64_t stride = uint64_t(gridDim.x) * 256;
+  for (uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x; t < a.n4; t += stride)
+  {
+    f4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = NTL ? __builtin_nontemporal_load(&a.in[k][t]) : a.in[k][t];
+    f4 s = v[0];
+    s.x += v[3].x; s.y += v[4].y; s.z += v[5].z; s.w += v[1].w + v[2].x;
+    if (NTS)
+    {
+      __builtin_nontemporal_store(s, &a.out[0][t]); __builtin_nontemporal_store(v[1], &a.out[1][t]);
+      __builtin_nontemporal_store(v[2], &a.out[2][t]); __builtin_nontemporal_store(v[4], &a.out[3][t]);
+    }
+    else { a.out[0][t] = s; a.out[1][t] = v[1]; a.out[2][t] = v[2]; a.out[3][t] = v[4]; }
+  }
+}
+
 extern "C" int roofprobe(int variant, const float* const* in, float* const* out, uint64_t n, int blocks, void* stream)
 {
   Args a;
@@ -234,6 +256,8 @@ extern "C" int roofprobe(int variant, const float* const* in, float* const* out,
     case 12: hipLaunchKernelGGL(k_probe_aos<12>, dim3(blocks), dim3(256), 0, s, a); break;
     case 13: hipLaunchKernelGGL(k_probe_aos<13>, dim3(blocks), dim3(256), 0, s, a); break;
     case 14: hipLaunchKernelGGL(k_probe_aos<14>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 15: hipLaunchKernelGGL((k_probe_mix<true, false>), dim3(blocks), dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_probe_mix<false, true>), dim3(blocks), dim3(256), 0, s, a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;

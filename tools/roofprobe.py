@@ -17,11 +17,12 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-BYTES = {0: 40, 1: 40, 2: 40, 3: 24, 4: 16, 5: 8, 6: 40, 7: 24, 8: 16, 9: 40, 10: 40, 11: 40, 12: 40, 13: 40, 14: 40}
+BYTES = {0: 40, 1: 40, 2: 40, 3: 24, 4: 16, 5: 8, 6: 40, 7: 24, 8: 16, 9: 40, 10: 40, 11: 40, 12: 40, 13: 40, 14: 40, 15: 40, 16: 40}
 NAMES = {0: "plain 6in/4out", 1: "nontemporal 6in/4out", 2: "8 pairs/thread 6in/4out", 3: "read-only 6in",
          4: "write-only 4out", 5: "copy nt 1in/1out", 6: "nt 2 quads/lane 6in/4out", 7: "read-only nt 6in",
          8: "write-only nt 4out", 9: "nt chunk 16 tiles/WG", 10: "nt chunk 64 tiles/WG", 11: "nt chunk 4 tiles/WG",
-         12: "AoS pair/lane", 13: "AoS 4 pairs/lane", 14: "AoS 4 pairs wave-strided"}
+         12: "AoS pair/lane", 13: "AoS 4 pairs/lane", 14: "AoS 4 pairs wave-strided",
+         15: "nt loads, plain stores", 16: "plain loads, nt stores"}
 
 
 def main():
@@ -49,7 +50,7 @@ def main():
     for v in [int(x) for x in os.environ.get("PROBE_VARIANTS", "0,1,2,3,4,5,6,7,8").split(",")]:
         for blocks in (1024, 2048, 4096, 8192, 16384, (n // 4 + 255) // 256):
             for _ in range(2):
-                ip, op = (aos_in_ptrs, aos_out_ptrs) if v >= 12 else (in_ptrs, out_ptrs)
+                ip, op = (aos_in_ptrs, aos_out_ptrs) if 12 <= v <= 14 else (in_ptrs, out_ptrs)
                 assert lib.roofprobe(v, ip, op, n, blocks, s.cuda_stream) == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
