@@ -148,12 +148,7 @@ __device__ __forceinline__ float4 ld4(const float* p, uint64_t t)
 template<bool NT>
 __device__ __forceinline__ void st4(float* p, uint64_t t, float a, float b, float c, float d)
 {
-#ifdef BBM_HIP_PLAIN_STORES
-  if (false)           // A/B: nontemporal loads with plain stores
-#else
-  if (NT)
-#endif
-    __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
+  if (NT) __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + t);
   else reinterpret_cast<float4*>(p)[t] = make_float4(a, b, c, d);
 }
 
