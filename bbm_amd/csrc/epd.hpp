@@ -14,6 +14,7 @@
 // (bbm::toString(float) = ostream << float).  tests/test_gpu_parity.py compares the result with the
 // reference's own table entry by entry.
 #pragma once
+#include <cmath>
 #include "math.hpp"
 #include "microfacet.hpp"
 #include "fit.hpp"     // phi_of
@@ -49,8 +50,10 @@ __device__ __forceinline__ float epd_g1_lookup(const float* tab, float p, float 
   // instructions each): m1 only places the bilinear weights, which are continuous across a floor() flip, so an
   // m1 within 1e-12 of the reference's moves the interpolated G1 by ~1e-12 relative
   // (L = +-inf at t = 0 / inf: the reference's exp(-exp(L 0.05)) is 0 / 1, exp_dd's polynomial would give NaN)
-#ifdef BBM_HIP_EPD_LOGF_CR
+#if defined(BBM_HIP_EPD_LOGF_CR)
   const double L = double(logf_cr(div_nr(1.0f, t)));
+#elif defined(BBM_HIP_EPD_LOGF_GLIBC)
+  const double L = double(logf_glibc(div_nr(1.0f, t)));      // A/B: glibc's logf, bit for bit
 #else
   // ln(1 / t) from log2_acc (~2^-44 absolute) instead of the library's double log: like m1's exponentials it only
   // places the bilinear weights, continuously (dm1/dL <= ~18.4), so ~1e-13 in L moves G1 by ~1e-12 relative
@@ -167,20 +170,42 @@ struct EpdNdf
 {
   static constexpr int kParams = 2;
   float beta, p, normalization, inv_p;
+  // The slots after EPD's parameters (EpdM: 4, 5): glibc's tgammaf(1 / p) computed on the host (host_params<EpdM>)
+  // and the p it belongs to.  glibc 2.35's tgammaf is not correctly rounded (it differs from the correctly rounded
+  // float on 27 % of the floats in [0.19, 5.1]) and the device library's is a third function again: a normalization
+  // an ulp off moved D, and with it eval and pdf, by an ulp on ~4 % of the lanes of a set (EPD[2] of the golden
+  // sets).  Where no host value rides along (a probe of the fitting loss, whose parameters are made on the device)
+  // the correctly rounded tgamma of the double.
+  static constexpr int kGammaSlot = 4;
   __device__ explicit EpdNdf(const float* q) : beta(q[0]), p(q[1])
   {
     // compute_normalization (epd.h:160-178): p InvPi rcp(tgamma(rcp(p))) / beta^2, 0 if p <= eps
-    const float n = (p > kEpsF) ? (p * kInvPiF) * div_nr(1.0f, tgammaf(div_nr(1.0f, p))) : 0.0f;
+    uint32_t tag, pb;
+    __builtin_memcpy(&tag, q + kGammaSlot + 1, 4);
+    __builtin_memcpy(&pb, &p, 4);
+    const float g = (tag == pb && pb != 0u) ? q[kGammaSlot] : float(tgamma(double(div_nr(1.0f, p))));
+    const float n = (p > kEpsF) ? (p * kInvPiF) * div_nr(1.0f, g) : 0.0f;
     normalization = div_nr(n, beta * beta);
     inv_p = div_nr(1.0f, p);
   }
 
-  // epd.h:56-73: normalization exp(-pow(tan^2 / beta^2, p)) / cos^4, masked z(h) > 0
+  // epd.h:56-73: normalization exp(-pow(tan^2 / beta^2, p)) / cos^4, masked z(h) > 0.  The power is glibc's powf to
+  // its last bit (math.hpp): the exponential amplifies a 1-ulp power into x ulps of D (x = the power, up to ~100
+  // where D is still normal), and powf_acc -- correctly rounded, where glibc's powf is not always -- left lanes up
+  // to 109 ulp apart (7.7e-6 relative) on a rough, high-p parameter set
+  __device__ __forceinline__ static float pw(float x, float y)
+  {
+#ifdef BBM_HIP_EPD_POWF_ACC
+    return powf_acc(x, y);              // A/B: the correctly rounded power
+#else
+    return powf_glibc<true>(x, y);
+#endif
+  }
   __device__ __forceinline__ float eval(v3 h) const
   {
     const float c2 = h.z * h.z;
     const float t2 = div_nr(1 - c2, c2);
-    const float D = div_nr(normalization * expf_lobe(-powf_acc(div_nr(t2, beta * beta), p)), c2 * c2);
+    const float D = div_nr(normalization * expf_lobe(-pw(div_nr(t2, beta * beta), p)), c2 * c2);
     return (h.z > 0) ? D : 0.0f;
   }
 
@@ -273,5 +298,18 @@ using EpdM = Microfacet<EpdNdf, VanGinneken, FresnelComplex, Norm::Walter, false
 // Builds the G1 table on the current device once (inst_epd.hip) and points g_epd_g1 at it.
 int epd_prepare(hipStream_t s);
 template<> struct host_prepare<EpdM> { static int run(hipStream_t s) { return epd_prepare(s); } };
+// the host's (glibc's) tgammaf(1 / p) for the normalization, and the p it was computed for (EpdNdf::kGammaSlot)
+template<> struct host_params<EpdM>
+{
+  static_assert(EpdM::kParams == EpdNdf::kGammaSlot, "EPD's gamma slots follow its parameters");
+  static int run(ParamBlock& q, uint32_t, hipStream_t, void**)
+  {
+    const float p = q.v[1];
+    q.v[EpdNdf::kGammaSlot] = std::tgamma(1.0f / p);      // tgammaf: float argument, float result
+    __builtin_memcpy(&q.v[EpdNdf::kGammaSlot + 1], &p, 4);
+    return 0;
+  }
+  static void done(void*, hipStream_t) {}
+};
 
 }  // namespace bbmhip
