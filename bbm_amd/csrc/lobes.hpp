@@ -11,15 +11,6 @@
 
 namespace bbmhip {
 
-// powf(x, 3.0f): x^2 exact as an f32 pair, one fused multiply-add -> the nearest float to x^3
-// (what a correctly rounded powf returns) except within ~2^-24 ulp of a midpoint
-__device__ __forceinline__ float cube_f(float x)
-{
-  float hi, lo;
-  two_prod(x, x, hi, lo);
-  return __builtin_fmaf(hi, x, lo * x);
-}
-
 // reflect(out, m) = m * dot(m, out) * 2.0 - out (core/vec_transform.h:43-44), float-exact form
 __device__ __forceinline__ v3 reflect_about(v3 out, v3 m)
 {
@@ -80,7 +71,10 @@ struct Ward
       if (KIND == 0) nf = kPi4F * sqrtf(in.z * out.z) * rx * ry;
       else if (KIND == 1) nf = kPi4F * rx * ry * (in.z * out.z);
       else nf = f_div_d(double(kPi4F * rx * ry) * (double(zH2) * double(zH2)), double(dot3(H, H)));
-      const float f = div_nr(expf_lobe(-exponent), nf);
+      // the exponential is subnormal on the lobe's far tail while the quotient is normal (nf < 1): div_sub<true> keeps
+      // that quotient the IEEE one, where div_nr's f32 remainder is rounded to the subnormal grid (3/4 of the lanes
+      // that were an ulp off, profiles/r06_ward_bitexact.txt); Ward is HBM-bound, the f64 remainder step is free
+      const float f = div_sub<true>(expf_lobe(-exponent), nf);
       rgb[0] = active ? albedo[0] * f : 0.0f;
       rgb[1] = active ? albedo[1] * f : 0.0f;
       rgb[2] = active ? albedo[2] * f : 0.0f;
@@ -89,9 +83,10 @@ struct Ward
     if (MODE & kModePdf)
     {
       const v3 h = halfway(in, out);
-      const float nf = kPi4F * rx * ry * dot3(in, h) * cube_f(h.z);
+      // pow(cosTheta(h), 3) is glibc's powf, which is not always the correctly rounded cube (cube_f)
+      const float nf = kPi4F * rx * ry * dot3(in, h) * powf_glibc<true>(h.z, 3.0f);
       const float exponent = div_nr(sqnorm2(div_nr(h.x, rx), div_nr(h.y, ry)), h.z * h.z);
-      const float p = div_nr(expf_lobe(-exponent), nf);
+      const float p = div_sub<true>(expf_lobe(-exponent), nf);
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;
