@@ -74,7 +74,8 @@ struct Ward
       // the exponential is subnormal on the lobe's far tail while the quotient is normal (nf < 1): div_sub<true> keeps
       // that quotient the IEEE one, where div_nr's f32 remainder is rounded to the subnormal grid (3/4 of the lanes
       // that were an ulp off, profiles/r06_ward_bitexact.txt); Ward is HBM-bound, the f64 remainder step is free
-      const float f = div_sub<true>(expf_lobe(-exponent), nf);
+      const float e = expf_lobe(-exponent);
+      const float f = (nf > 0.0f) ? div_sub<true>(e, nf) : div_nr(e, nf);    // nf = 0: IEEE x / 0 (div_nr)
       rgb[0] = active ? albedo[0] * f : 0.0f;
       rgb[1] = active ? albedo[1] * f : 0.0f;
       rgb[2] = active ? albedo[2] * f : 0.0f;
@@ -86,7 +87,8 @@ struct Ward
       // pow(cosTheta(h), 3) is glibc's powf, which is not always the correctly rounded cube (cube_f)
       const float nf = kPi4F * rx * ry * dot3(in, h) * powf_glibc<true>(h.z, 3.0f);
       const float exponent = div_nr(sqnorm2(div_nr(h.x, rx), div_nr(h.y, ry)), h.z * h.z);
-      const float p = div_sub<true>(expf_lobe(-exponent), nf);
+      const float e = expf_lobe(-exponent);
+      const float p = (nf > 0.0f) ? div_sub<true>(e, nf) : div_nr(e, nf);    // cos^3 underflowed: IEEE x / 0
       pdf = active ? p : 0.0f;
     }
     else pdf = 0.0f;

@@ -144,7 +144,9 @@ __device__ __forceinline__ float div_nr(float n, float d)
 // of a far-tail halfway vector and the two quotients downstream of it); EXACT = false is div_nr.  Selected per
 // launch (bbm_hip_set_exact_subnormals): measured +3.6-4.3 % on the headline kernel (0.703 -> 0.734, 0.726 -> 0.752 ms per 100 M pairs),
 // CookTorrance eval+pdf then bit-identical to the reference on every lane of the 1 M-pair batches.  d = 0 / inf /
-// NaN give the IEEE quotient.
+// NaN give inf / NaN, which those sites select away (or guard: Ward's pdf).  (Widening the fallback below to NaN
+// and infinite quotients was tried in round 6: the fused Aggregate(Lambertian, NganHe) kernel then faulted on the
+// GPU -- an illegal address, results permuted -- so the IEEE special cases stay with the callers.)
 template<bool EXACT>
 __device__ __forceinline__ float div_sub(float n, float d)
 {
@@ -158,10 +160,7 @@ __device__ __forceinline__ float div_sub(float n, float d)
     // -- so those lanes (a wave-uniform branch, rarely taken) take the IEEE double quotient instead, which rounds to
     // the float grid exactly as the float division (53 >= 2 x 24 + 2, and a tie is exact in double).  Found by the
     // exhaustive device sweep of erfcf (tests/test_gpu_libm.py: erfcf(10) = 1.5 x 2^-149 rounded to even).
-    // The same fallback serves the IEEE special cases (d = 0, inf or NaN, an infinite n): the remainder step's
-    // NaN / inf there becomes the IEEE quotient (x / 0 = inf, e.g. Ward's pdf where cos^3 of the halfway vector
-    // underflows to 0).
-    const bool sub = !(__builtin_fabsf(q) >= 0x1p-126f) || __builtin_isinf(q);
+    const bool sub = __builtin_fabsf(q) < 0x1p-126f;
     if (__builtin_amdgcn_ballot_w64(sub) != 0)
       if (sub) q = float(double(n) / double(d));
     return q;
