@@ -73,6 +73,16 @@ __device__ __forceinline__ float theta_of(v3 v)
   return float(u);
 }
 
+// sgd_base::eval x K for a channel whose (alpha, p) lies outside the attributes' range: IEEE quotients, glibc's powf
+// with its negative-base and special-operand rules, expf with overflow.  Out of line for the eval kernels: inlined into
+// the channel block its code cost Bagher's eval 15 % although no valid launch runs it (profiles/r06_ab_bagher_range.txt).
+static __device__ __attribute__((noinline)) float p22_general(float alpha, float p, float tan2)
+{
+  const float t = alpha + tan2 / alpha;
+  const float den = powf_glibc_any(t, p);
+  return (den > kEpsF) ? expf_glibc(-t) / den : 0.0f;
+}
+
 struct Bagher
 {
   static constexpr bool kHasGeo = true;      // geometry() / eval_geo(): the loss kernel shares the prelude per pair
@@ -208,12 +218,17 @@ struct Bagher
         // sgd_base::eval (sgd.h:48-63) x K (sgd.h:143-154): exp(-t) / t^p with t = alpha + tan^2 / alpha
         if (!(alpha[j] >= 0x1p-126f && alpha[j] < __builtin_inff() && __builtin_isfinite(p[j]))) [[unlikely]]
         {
-          // a parameter outside the attribute's range (the reference accepts any alpha / p): the general forms --
-          // IEEE quotients, glibc's powf with its negative-base and special-operand rules, expf with overflow.  The
-          // parameters are uniform per launch (per probe in the loss), so this branch never splits a wave.
-          const float t = alpha[j] + g.tan2 / alpha[j];
-          const float den = powf_glibc_any(t, p[j]);
-          P22[j] = (den > kEpsF) ? expf_glibc(-t) / den : 0.0f;
+          // a parameter outside the attribute's range (the reference accepts any alpha / p): the general forms, out
+          // of line in the eval kernels (p22_general) and inline in the loss kernels (CACHE), where the call cost the
+          // config-5 step 19 %.  The parameters are uniform per launch (per probe in the loss), so this branch never
+          // splits a wave.
+          if constexpr (CACHE)
+          {
+            const float t = alpha[j] + g.tan2 / alpha[j];
+            const float den = powf_glibc_any(t, p[j]);
+            P22[j] = (den > kEpsF) ? expf_glibc(-t) / den : 0.0f;
+          }
+          else P22[j] = p22_general(alpha[j], p[j], g.tan2);
           continue;                                              // (never cached: only valid parameters fill it)
         }
         const float t = alpha[j] + div_nr(g.tan2, alpha[j]);
